@@ -1,0 +1,177 @@
+/*
+ * pycsou_hip.h -- C ABI of libpycsou_hip.so, the gfx950 (MI355X) engine behind
+ * the pycsou PrimalDualSplitting / APGD hot path.
+ *
+ * Conventions
+ *  - Buffers are caller-allocated DEVICE pointers, contiguous, C order (the
+ *    flat-vector layout pycsou uses: a d-dimensional image of `shape` is the
+ *    C-order ravel; a gradient is the concatenation [d_0 x; d_1 x; (d_2 x)],
+ *    pycsou/linop/diff.py:855-875).
+ *  - `dtype` is PCS_F32 or PCS_F64.  Scalars are passed as double and rounded
+ *    to `dtype` inside, exactly as NumPy does for `array * python_float`.
+ *  - Every entry point returns PCS_OK (0) or a negative status; nothing is
+ *    thrown across the ABI.  No entry point allocates, frees or synchronises:
+ *    all of them are hipGraph-capturable on `stream`.
+ *  - Workspaces (`ws`) are caller-allocated device buffers of the size the
+ *    matching *_ws_bytes() query returns.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * dhamm97/pycsou; PyLops 1.x for the operators pycsou delegates to it).
+ */
+#ifndef PYCSOU_HIP_H
+#define PYCSOU_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { PCS_F32 = 0, PCS_F64 = 1 };
+enum { PCS_OK = 0, PCS_EINVAL = -1, PCS_ELAUNCH = -2, PCS_EUNSUPPORTED = -3 };
+/* derivative kinds (pycsou/linop/diff.py:24 `kind`) */
+enum { PCS_FORWARD = 0, PCS_BACKWARD = 1, PCS_CENTERED = 2 };
+/* H functional kinds in the fused step */
+enum { PCS_H_L1 = 0, PCS_H_L21 = 1 };
+/* G functional kinds in the fused step */
+enum { PCS_G_NULL = 0, PCS_G_NONNEG = 1, PCS_G_SEGMENT = 2 };
+/* F kinds in the fused step */
+enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3 };
+
+int pcs_abi_version(void);
+
+/* ---------------------------------------------------------------- operators */
+
+/* FirstDerivative along `axis` (pycsou/linop/diff.py:24-130 -> pylops.FirstDerivative):
+ * out = D_axis x.  ndim in 1..3, dims[ndim], step = sampling. */
+int pcs_deriv1_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step,
+                   int kind, int edge, hipStream_t stream);
+/* Adjoint of the above (pylops FirstDerivative.rmatvec). */
+int pcs_deriv1_adj(int dtype, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step,
+                   int kind, int edge, hipStream_t stream);
+
+/* Gradient (pycsou/linop/diff.py:777-882 -> pylops.Gradient = VStack of FirstDerivative):
+ * out[k*N:(k+1)*N] = D_k x for k < ndim.  steps[ndim]. */
+int pcs_grad_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, const double* steps,
+                 int kind, int edge, hipStream_t stream);
+/* Gradient.adjoint: out = sum_k D_k^T z_k (accumulated in axis order, pylops VStack.rmatvec). */
+int pcs_grad_adj(int dtype, const void* z, void* out, int ndim, const int64_t* dims, const double* steps,
+                 int kind, int edge, hipStream_t stream);
+
+/* Laplacian 2-D (pycsou/linop/diff.py:885-957 -> pylops.Laplacian):
+ * out = w0 * D2_0 x + w1 * D2_1 x.  dims[2], weights[2], steps[2]. */
+int pcs_lap_fwd(int dtype, const void* x, void* out, const int64_t* dims, const double* weights,
+                const double* steps, int edge, hipStream_t stream);
+int pcs_lap_adj(int dtype, const void* y, void* out, const int64_t* dims, const double* weights,
+                const double* steps, int edge, hipStream_t stream);
+
+/* Convolve2D (pycsou/linop/conv.py:167-295 -> pylops Convolve2D, 'same', zero boundary):
+ * out[i] = sum_j h[j] x[i + off - j] (+ beta * b[i] if b != NULL).  `psf` is a device
+ * buffer kh*kw of dtype.  The adjoint (correlation) is this call with the flipped PSF
+ * and offsets (kh-1-off0, kw-1-off1). */
+int pcs_conv2d(int dtype, const void* x, void* out, int64_t n0, int64_t n1, const void* psf, int kh, int kw,
+               int off0, int off1, const void* b, double beta, hipStream_t stream);
+
+/* Convolve1D along `axis` of a 1..3-D array (pycsou/linop/conv.py:20-164 -> pylops Convolve1D):
+ * out[i] = sum_t h[t] x[i + (off - t) e_axis].  Adjoint = flipped taps, off' = k-1-off. */
+int pcs_conv1d(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps,
+               int k, int off, hipStream_t stream);
+
+/* ---------------------------------------------------------------- prox / functionals */
+
+/* L1Norm.prox (pycsou/func/penalty.py:194-245 via LpNorm.prox, func/base.py:239-240):
+ * out = x - tau*clip(x/tau, -1, 1). */
+int pcs_prox_l1(int dtype, const void* x, void* out, int64_t n, double tau, hipStream_t stream);
+/* (lam*L1Norm).fenchel_prox (core/functional.py:207, 264-265):
+ * out = w - sigma * prox_l1(w/sigma, (1/sigma)*lam). */
+int pcs_fenchel_l1(int dtype, const void* w, void* out, int64_t n, double sigma, double lam, hipStream_t stream);
+/* L21Norm.prox with pixel groups tile(arange(npix), d) (func/penalty.py:551-557):
+ * out_g = max(1 - tau/||x_g||, 0) x_g. */
+int pcs_prox_l21_pixel(int dtype, const void* x, void* out, int64_t npix, int d, double tau, hipStream_t stream);
+int pcs_fenchel_l21_pixel(int dtype, const void* w, void* out, int64_t npix, int d, double sigma, double lam,
+                          hipStream_t stream);
+/* L21Norm.prox with arbitrary labels: `gid[n]` = index of the element's group in
+ * [0, ngroups) (np.unique order); ws = ngroups doubles. */
+int pcs_prox_l21_labels(int dtype, const void* x, void* out, int64_t n, const int32_t* gid, int64_t ngroups,
+                        double tau, void* ws, hipStream_t stream);
+/* L2Norm.prox (func/penalty.py:23-70 via LpNorm.prox + proj_l2_ball, math/prox.py:207-210):
+ * v = x/tau; out = x - tau*(||v|| <= 1 ? v : v/||v||), with ||x||^2 read from the device
+ * double `sumsq_dev` (pcs_reduce kind 0). */
+int pcs_prox_l2(int dtype, const void* x, void* out, int64_t n, double tau, const double* sumsq_dev,
+                hipStream_t stream);
+/* SquaredL2Norm prox (new API, core/functional.py:100-103): out = x / (1 + 2 tau). */
+int pcs_prox_sql2(int dtype, const void* x, void* out, int64_t n, double tau, hipStream_t stream);
+/* NonNegativeOrthant / Segment projections (math/prox.py:295-297, 340-343). */
+int pcs_proj_nonneg(int dtype, const void* x, void* out, int64_t n, hipStream_t stream);
+int pcs_proj_segment(int dtype, const void* x, void* out, int64_t n, double a, double b, hipStream_t stream);
+
+/* ---------------------------------------------------------------- algebra / reductions */
+
+/* out = a*x + b*y (y may be NULL -> out = a*x).  Numpy-order: (a*x) + (b*y). */
+int pcs_axpby(int dtype, const void* x, const void* y, void* out, int64_t n, double a, double b,
+              hipStream_t stream);
+/* out = (x - a*y) - b*w  (the PDS primal argument, proxalgs.py:348). */
+int pcs_sub2(int dtype, const void* x, const void* y, const void* w, void* out, int64_t n, double a, double b,
+             hipStream_t stream);
+/* Deterministic fp64 reductions into out_dev[0]: kind 0 = sum x^2, 1 = sum |x|,
+ * 2 = sum (x-y)^2, 3 = sum x*y.  ws >= pcs_reduce_ws_bytes(). */
+int64_t pcs_reduce_ws_bytes(void);
+int pcs_reduce(int dtype, int kind, const void* x, const void* y, int64_t n, double* out_dev, void* ws,
+               hipStream_t stream);
+
+/* ---------------------------------------------------------------- fused PDS iteration */
+
+/* One fused PrimalDualSplitting.update_iterand + update_diagnostics
+ * (pycsou/opt/proxalgs.py:343-394) for 2-D images, K = Gradient(kind='forward'):
+ *   g   = grad F(x)           (F kind: 0, x - y, Conv^T(Conv x - y) separable, or read from gbuf)
+ *   x_t = prox_G((x - tau g) - tau K^T z)
+ *   u   = 2 x_t - x
+ *   z_t = H.fenchel_prox(z + sigma K u, sigma)      (H = lam*L1 or lam*L21 pixel groups)
+ *   z'  = rho z_t + (1-rho) z ;  x' = rho x_t + (1-rho) x
+ * plus per-block partials of ||x-x'||^2, ||x||^2, ||z-z'||^2, ||z||^2.
+ * Slab form: the local arrays hold rows [row0 - halo, row0 + rows + halo) of a
+ * global n0 x n1 image (halo rows of x: pcs_pds2d_halo_x, of z: 2, of y: halo_x/2+1). */
+typedef struct {
+  int dtype;          /* PCS_F32 / PCS_F64 */
+  int fkind;          /* PCS_F_* */
+  int hkind;          /* PCS_H_* */
+  int gkind;          /* PCS_G_* */
+  int64_t n0, n1;     /* global image */
+  int64_t row0, rows; /* this slab: global rows [row0, row0+rows) */
+  int halo_x, halo_z, halo_y; /* halo rows stored above/below the slab in x/xn, z/zn, y/gbuf */
+  int half;           /* separable conv half width H (taps 2H+1, centred) */
+  const void* taps0;  /* 2H+1 taps along axis 0 (rows), device */
+  const void* taps1;  /* 2H+1 taps along axis 1 (cols), device */
+  double tau, sigma, rho, lam, step0, step1, seg_a, seg_b;
+  const void* x; void* xn; const void* z; void* zn; const void* y; const void* gbuf;
+  double* partials;       /* [nblocks][4] */
+  const int32_t* ctrl;    /* device control block (pcs_ctrl_*) ; NULL = always run */
+} pcs_pds2d_args;
+
+int pcs_pds2d_halo_x(int half);
+int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
+int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
+
+/* Device control block for the hipGraph-captured loop:
+ * int32 [0]=it (next iteration), [1]=stopped, [2]=min_iter, [3]=max_iter, [4]=has_dual,
+ * [5]=hist_len; double at byte 32: accuracy_threshold.
+ * hist: double[2*(max(min_iter,max_iter)+1)+2] = (primal, dual) relative improvement per iteration. */
+int64_t pcs_ctrl_bytes(void);
+int pcs_ctrl_init(void* ctrl_dev, int min_iter, int max_iter, double thr, int has_dual, hipStream_t stream);
+/* Reduce [nparts][4] partials (fixed order, fp64) into sums[4]. */
+int pcs_reduce_partials(const double* partials, int64_t nparts, double* sums, hipStream_t stream);
+/* From sums[4] (global), write hist[it], advance it, set stopped per
+ * GenericIterativeAlgorithm.iterate's loop condition (pycsou/core/solver.py:65-66). */
+int pcs_pds_finalize(const double* sums, void* ctrl_dev, double* hist, hipStream_t stream);
+/* Single-GPU shortcut: pcs_reduce_partials + pcs_pds_finalize in one launch. */
+int pcs_pds_reduce_finalize(const double* partials, int64_t nparts, void* ctrl_dev, double* hist,
+                            hipStream_t stream);
+/* pcs_ctrl_init with an explicit history length (doubles in `hist`). */
+int pcs_ctrl_init2(void* ctrl_dev, int min_iter, int max_iter, double thr, int has_dual, int hist_len,
+                   hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PYCSOU_HIP_H */

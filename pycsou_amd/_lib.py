@@ -1,0 +1,135 @@
+"""ctypes binding of libpycsou_hip.so (the C ABI declared in include/pycsou_hip.h).
+
+There is exactly one compute path: the gfx950 HIP kernels in this library.  If the
+library is missing or no ROCm GPU is visible, every compute call raises -- there is
+no NumPy / PyTorch fallback.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must be imported first: its libamdhip64.so.7 is the one we bind to
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'lib', 'libpycsou_hip.so')
+
+PCS_F32, PCS_F64 = 0, 1
+PCS_FORWARD, PCS_BACKWARD, PCS_CENTERED = 0, 1, 2
+PCS_H_L1, PCS_H_L21 = 0, 1
+PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
+PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF = 0, 1, 2, 3
+KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
+
+_c_int, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_pdbl = ctypes.POINTER(ctypes.c_double)
+
+
+class PdsArgs(ctypes.Structure):
+    """Mirror of pcs_pds2d_args."""
+    _fields_ = [('dtype', _c_int), ('fkind', _c_int), ('hkind', _c_int), ('gkind', _c_int),
+                ('n0', _c_i64), ('n1', _c_i64), ('row0', _c_i64), ('rows', _c_i64),
+                ('halo_x', _c_int), ('halo_z', _c_int), ('halo_y', _c_int), ('half', _c_int),
+                ('taps0', _vp), ('taps1', _vp),
+                ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
+                ('step0', _c_dbl), ('step1', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
+                ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
+                ('partials', _vp), ('ctrl', _vp)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    'pcs_abi_version': (_c_int, []),
+    'pcs_deriv1_fwd': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _c_int, _vp]),
+    'pcs_deriv1_adj': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _c_int, _vp]),
+    'pcs_grad_fwd': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _pdbl, _c_int, _c_int, _vp]),
+    'pcs_grad_adj': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _pdbl, _c_int, _c_int, _vp]),
+    'pcs_lap_fwd': (_c_int, [_c_int, _vp, _vp, _pi64, _pdbl, _pdbl, _c_int, _vp]),
+    'pcs_lap_adj': (_c_int, [_c_int, _vp, _vp, _pi64, _pdbl, _pdbl, _c_int, _vp]),
+    'pcs_conv2d': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_dbl,
+                            _vp]),
+    'pcs_conv1d': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _vp, _c_int, _c_int, _vp]),
+    'pcs_prox_l1': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp]),
+    'pcs_fenchel_l1': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
+    'pcs_prox_l21_pixel': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_int, _c_dbl, _vp]),
+    'pcs_fenchel_l21_pixel': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_int, _c_dbl, _c_dbl, _vp]),
+    'pcs_prox_l21_labels': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp, _c_i64, _c_dbl, _vp, _vp]),
+    'pcs_prox_l2': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp, _vp]),
+    'pcs_prox_sql2': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp]),
+    'pcs_proj_nonneg': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
+    'pcs_proj_segment': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
+    'pcs_axpby': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
+    'pcs_sub2': (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
+    'pcs_reduce_ws_bytes': (_c_i64, []),
+    'pcs_reduce': (_c_int, [_c_int, _c_int, _vp, _vp, _c_i64, _vp, _vp, _vp]),
+    'pcs_pds2d_halo_x': (_c_int, [_c_int]),
+    'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
+    'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
+    'pcs_ctrl_bytes': (_c_i64, []),
+    'pcs_ctrl_init': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _vp]),
+    'pcs_ctrl_init2': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _c_int, _vp]),
+    'pcs_reduce_partials': (_c_int, [_vp, _c_i64, _vp, _vp]),
+    'pcs_pds_finalize': (_c_int, [_vp, _vp, _vp, _vp]),
+    'pcs_pds_reduce_finalize': (_c_int, [_vp, _c_i64, _vp, _vp, _vp]),
+}
+
+EXPORTS = tuple(_SIGS)
+_lib = None
+
+
+class HipError(ValueError):
+    """A C-ABI entry point returned a nonzero status (the reference raises ValueError
+    for invalid shapes/parameters; launch failures are reported the same way)."""
+
+
+def load():
+    """Load and declare the library (no GPU needed to load it)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'pycsou_amd: {LIB_PATH} is not built -- run `make` (or __graft_entry__.build()). '
+                               'There is no CPU fallback.')
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = lib
+    return _lib
+
+
+def gpu():
+    """Library handle for a compute call: requires a visible ROCm GPU."""
+    lib = load()
+    if not torch.cuda.is_available():
+        raise RuntimeError('pycsou_amd: no ROCm GPU is visible; the gfx950 HIP kernels are the only compute path.')
+    return lib
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def check(rc, name):
+    if rc != 0:
+        raise HipError(f'{name} returned status {rc}')
+    return rc
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def i64s(vals):
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
+def dbls(vals):
+    return (ctypes.c_double * len(vals))(*[float(v) for v in vals])
+
+
+def dtcode(t):
+    if t.dtype == torch.float32:
+        return PCS_F32
+    if t.dtype == torch.float64:
+        return PCS_F64
+    raise TypeError(f'pycsou_amd kernels support float32/float64, got {t.dtype}')

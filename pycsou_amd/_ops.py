@@ -1,0 +1,256 @@
+"""Tensor-level wrappers over the C ABI + the array boundary of the public API.
+
+Public pycsou-style methods accept NumPy arrays or torch tensors and return the same
+kind they were given (NumPy in -> NumPy out, as in the reference; torch in -> device
+tensor out).  Everything in between is a contiguous 1-D device tensor handled by the
+gfx950 kernels.
+"""
+
+from numbers import Number
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_ws_cache = {}
+
+
+# ---------------------------------------------------------------- array boundary
+
+def device():
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def torch_dtype(dtype, default=torch.float64):
+    if dtype is None:
+        return default
+    if isinstance(dtype, torch.dtype):
+        return dtype
+    d = np.dtype(dtype)
+    if d == np.float32:
+        return torch.float32
+    return torch.float64
+
+
+def to_dev(x, dtype=None):
+    """Contiguous flat device tensor (float32/float64) from NumPy / torch / scalar."""
+    L.gpu()
+    if isinstance(x, torch.Tensor):
+        t = x
+        if dtype is None and t.dtype not in (torch.float32, torch.float64):
+            dtype = torch.float64
+        if dtype is not None and t.dtype != dtype:
+            t = t.to(dtype)
+        if not t.is_cuda:
+            t = t.to(device())
+        return t.reshape(-1).contiguous()
+    a = np.asarray(x)
+    if dtype is None:
+        dtype = torch.float32 if a.dtype == np.float32 else torch.float64
+    return torch.as_tensor(np.ascontiguousarray(a).reshape(-1)).to(device=device(), dtype=dtype)
+
+
+def like(out, ref):
+    """Return `out` (device tensor) as the array kind of `ref`."""
+    if isinstance(ref, torch.Tensor):
+        return out
+    return out.detach().cpu().numpy()
+
+
+def numel(x):
+    return int(x.numel()) if isinstance(x, torch.Tensor) else int(np.size(x))
+
+
+def is_array(x):
+    return isinstance(x, (np.ndarray, torch.Tensor))
+
+
+def empty_like(t):
+    return torch.empty_like(t)
+
+
+# ---------------------------------------------------------------- elementwise / algebra
+
+def axpby(x, y, a, b, out=None):
+    """out = a*x + b*y  (y may be None)."""
+    lib = L.gpu()
+    out = torch.empty_like(x) if out is None else out
+    L.check(lib.pcs_axpby(L.dtcode(x), L.ptr(x), L.ptr(y), L.ptr(out), x.numel(), float(a), float(b),
+                          L.stream()), 'pcs_axpby')
+    return out
+
+
+def scale(x, a):
+    return axpby(x, None, a, 0.0)
+
+
+def add(x, y):
+    return axpby(x, y, 1.0, 1.0)
+
+
+def sub2(x, y, w, a, b):
+    """(x - a*y) - b*w  (proxalgs.py:348)."""
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_sub2(L.dtcode(x), L.ptr(x), L.ptr(y), L.ptr(w), L.ptr(out), x.numel(), float(a), float(b),
+                         L.stream()), 'pcs_sub2')
+    return out
+
+
+def _ws(t):
+    key = (t.device, 'reduce')
+    ws = _ws_cache.get(key)
+    if ws is None:
+        lib = L.gpu()
+        ws = torch.empty(int(lib.pcs_reduce_ws_bytes()) // 8 + 8, dtype=torch.float64, device=t.device)
+        _ws_cache[key] = ws
+    return ws
+
+
+def reduce_dev(kind, x, y=None, out=None):
+    """Deterministic fp64 reduction into a 1-element device tensor.
+    kind: 0 sum x^2, 1 sum |x|, 2 sum (x-y)^2, 3 sum x*y."""
+    lib = L.gpu()
+    out = torch.empty(1, dtype=torch.float64, device=x.device) if out is None else out
+    L.check(lib.pcs_reduce(L.dtcode(x), int(kind), L.ptr(x), L.ptr(y), x.numel(), L.ptr(out), L.ptr(_ws(x)),
+                           L.stream()), 'pcs_reduce')
+    return out
+
+
+def sumsq(x):
+    return float(reduce_dev(0, x).item())
+
+
+def norm(x):
+    return float(np.sqrt(sumsq(x)))
+
+
+# ---------------------------------------------------------------- prox
+
+def prox_l1(x, tau):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_prox_l1(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), float(tau), L.stream()), 'pcs_prox_l1')
+    return out
+
+
+def fenchel_l1(w, sigma, lam):
+    lib = L.gpu()
+    out = torch.empty_like(w)
+    L.check(lib.pcs_fenchel_l1(L.dtcode(w), L.ptr(w), L.ptr(out), w.numel(), float(sigma), float(lam), L.stream()),
+            'pcs_fenchel_l1')
+    return out
+
+
+def prox_l21_pixel(x, tau, d):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_prox_l21_pixel(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel() // d, int(d), float(tau),
+                                   L.stream()), 'pcs_prox_l21_pixel')
+    return out
+
+
+def fenchel_l21_pixel(w, sigma, lam, d):
+    lib = L.gpu()
+    out = torch.empty_like(w)
+    L.check(lib.pcs_fenchel_l21_pixel(L.dtcode(w), L.ptr(w), L.ptr(out), w.numel() // d, int(d), float(sigma),
+                                      float(lam), L.stream()), 'pcs_fenchel_l21_pixel')
+    return out
+
+
+def prox_l21_labels(x, tau, gid, ngroups):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    ws = torch.empty(int(ngroups), dtype=torch.float64, device=x.device)
+    L.check(lib.pcs_prox_l21_labels(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), L.ptr(gid), int(ngroups),
+                                    float(tau), L.ptr(ws), L.stream()), 'pcs_prox_l21_labels')
+    return out
+
+
+def prox_l2(x, tau):
+    lib = L.gpu()
+    ss = reduce_dev(0, x)
+    out = torch.empty_like(x)
+    L.check(lib.pcs_prox_l2(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), float(tau), L.ptr(ss), L.stream()),
+            'pcs_prox_l2')
+    return out
+
+
+def prox_sql2(x, tau):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_prox_sql2(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), float(tau), L.stream()),
+            'pcs_prox_sql2')
+    return out
+
+
+def proj_nonneg(x):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_proj_nonneg(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), L.stream()), 'pcs_proj_nonneg')
+    return out
+
+
+def proj_segment(x, a, b):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_proj_segment(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), float(a), float(b), L.stream()),
+            'pcs_proj_segment')
+    return out
+
+
+# ---------------------------------------------------------------- operators
+
+def grad_fwd(x, dims, steps, kind, edge):
+    lib = L.gpu()
+    out = torch.empty(len(dims) * x.numel(), dtype=x.dtype, device=x.device)
+    L.check(lib.pcs_grad_fwd(L.dtcode(x), L.ptr(x), L.ptr(out), len(dims), L.i64s(dims), L.dbls(steps),
+                             L.KINDS[kind], int(bool(edge)), L.stream()), 'pcs_grad_fwd')
+    return out
+
+
+def grad_adj(z, dims, steps, kind, edge):
+    lib = L.gpu()
+    out = torch.empty(z.numel() // len(dims), dtype=z.dtype, device=z.device)
+    L.check(lib.pcs_grad_adj(L.dtcode(z), L.ptr(z), L.ptr(out), len(dims), L.i64s(dims), L.dbls(steps),
+                             L.KINDS[kind], int(bool(edge)), L.stream()), 'pcs_grad_adj')
+    return out
+
+
+def deriv1(x, dims, axis, step, kind, edge, adjoint=False):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    fn = lib.pcs_deriv1_adj if adjoint else lib.pcs_deriv1_fwd
+    L.check(fn(L.dtcode(x), L.ptr(x), L.ptr(out), len(dims), L.i64s(dims), int(axis), float(step), L.KINDS[kind],
+               int(bool(edge)), L.stream()), 'pcs_deriv1')
+    return out
+
+
+def lap(x, dims, weights, steps, edge, adjoint=False):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    fn = lib.pcs_lap_adj if adjoint else lib.pcs_lap_fwd
+    L.check(fn(L.dtcode(x), L.ptr(x), L.ptr(out), L.i64s(dims), L.dbls(weights), L.dbls(steps), int(bool(edge)),
+               L.stream()), 'pcs_lap')
+    return out
+
+
+def conv2d(x, dims, psf_dev, kh, kw, off0, off1, b=None, beta=0.0):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_conv2d(L.dtcode(x), L.ptr(x), L.ptr(out), int(dims[0]), int(dims[1]), L.ptr(psf_dev), int(kh),
+                           int(kw), int(off0), int(off1), L.ptr(b), float(beta), L.stream()), 'pcs_conv2d')
+    return out
+
+
+def conv1d(x, dims, axis, taps_dev, k, off):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_conv1d(L.dtcode(x), L.ptr(x), L.ptr(out), len(dims), L.i64s(dims), int(axis), L.ptr(taps_dev),
+                           int(k), int(off), L.stream()), 'pcs_conv1d')
+    return out
+
+
+def scalar(x):
+    return isinstance(x, Number)

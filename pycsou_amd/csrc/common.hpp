@@ -1,0 +1,63 @@
+// Shared helpers for the gfx950 kernels behind include/pycsou_hip.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pycsou_hip.h"
+
+namespace pcs {
+
+constexpr int kWave = 64;
+
+// Launch-status helper: never synchronises (graph-capture safe).
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? PCS_OK : PCS_ELAUNCH;
+}
+
+inline unsigned grid_for(int64_t n, int block, unsigned cap = 8192) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > (int64_t)cap) g = cap;
+  return (unsigned)g;
+}
+
+template <typename T>
+__device__ __forceinline__ T clip1(T v) {
+  // proj_linfty_ball(v, 1): y[y>1]=1; y[y<-1]=-1 (NaN passes through)
+  // pycsou/math/prox.py:253-256
+  return v > T(1) ? T(1) : (v < T(-1) ? T(-1) : v);
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Block-wide sum of NV doubles; result valid in thread 0.  `sm` must hold
+// (blockDim/64)*NV doubles.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sm[w * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double s = 0.0;
+      for (int i = 0; i < nw; ++i) s += sm[i * NV + k];
+      v[k] = s;
+    }
+  }
+}
+
+}  // namespace pcs

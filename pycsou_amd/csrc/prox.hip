@@ -1,0 +1,281 @@
+// Proximal operators, projections, vector algebra and deterministic reductions.
+//
+// Replaces the NumPy bodies of pycsou/func/base.py:239-240 (LpNorm.prox),
+// pycsou/func/penalty.py:23-131, 480-668 (L2/SquaredL2/L1/L21 norms, indicator
+// projections), pycsou/core/functional.py:207, 264-265 (fenchel_prox, lambda*f),
+// pycsou/math/prox.py:167-343 (ball / orthant / segment projections) and the
+// np.linalg.norm calls of proxalgs.py:366-394.  All are HBM-bound streaming
+// kernels: grid-stride loops, one element per thread per trip.
+#include "common.hpp"
+
+namespace pcs {
+
+#define PCS_GRID_LOOP(p, n) \
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < (n); p += (int64_t)gridDim.x * blockDim.x)
+
+template <typename T>
+__device__ __forceinline__ T prox_l1_el(T v, T t) {
+  // x - tau * proj_linfty_ball(x / tau, 1)
+  return v - t * clip1(v / t);
+}
+
+template <typename T>
+__global__ void k_prox_l1(const T* __restrict__ x, T* __restrict__ out, int64_t n, T tau) {
+  PCS_GRID_LOOP(p, n) out[p] = prox_l1_el(x[p], tau);
+}
+
+template <typename T>
+__global__ void k_fenchel_l1(const T* __restrict__ w, T* __restrict__ out, int64_t n, T sigma, T t) {
+  // w - sigma * prox(w / sigma, t), t = (1/sigma)*lam
+  PCS_GRID_LOOP(p, n) {
+    const T v = w[p];
+    out[p] = v - sigma * prox_l1_el(v / sigma, t);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T l21_fac(T nrm, T t) {
+  // clip(1 - tau / ||x_g||, 0, None); tau/0 = inf -> 0 (penalty.py:554)
+  const T f = T(1) - t / nrm;
+  return f > T(0) ? f : T(0);
+}
+
+template <typename T>
+__global__ void k_prox_l21_pixel(const T* __restrict__ x, T* __restrict__ out, int64_t npix, int d, T tau) {
+  PCS_GRID_LOOP(p, npix) {
+    T s = T(0);
+    for (int k = 0; k < d; ++k) {
+      const T v = x[k * npix + p];
+      s += v * v;
+    }
+    const T f = l21_fac(sqrt(s), tau);
+    for (int k = 0; k < d; ++k) out[k * npix + p] = f * x[k * npix + p];
+  }
+}
+
+template <typename T>
+__global__ void k_fenchel_l21_pixel(const T* __restrict__ w, T* __restrict__ out, int64_t npix, int d, T sigma,
+                                    T t) {
+  PCS_GRID_LOOP(p, npix) {
+    T s = T(0);
+    for (int k = 0; k < d; ++k) {
+      const T v = w[k * npix + p] / sigma;
+      s += v * v;
+    }
+    const T f = l21_fac(sqrt(s), t);
+    for (int k = 0; k < d; ++k) {
+      const T wv = w[k * npix + p];
+      out[k * npix + p] = wv - sigma * (f * (wv / sigma));
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_group_sumsq(const T* __restrict__ x, const int32_t* __restrict__ gid, int64_t n,
+                              double* __restrict__ acc) {
+  PCS_GRID_LOOP(p, n) {
+    const double v = (double)x[p];
+    atomicAdd(&acc[gid[p]], v * v);
+  }
+}
+
+template <typename T>
+__global__ void k_group_scale(const T* __restrict__ x, const int32_t* __restrict__ gid, int64_t n,
+                              const double* __restrict__ acc, T tau, T* __restrict__ out) {
+  PCS_GRID_LOOP(p, n) {
+    const T f = l21_fac((T)sqrt(acc[gid[p]]), tau);
+    out[p] = f * x[p];
+  }
+}
+
+template <typename T>
+__global__ void k_prox_l2(const T* __restrict__ x, T* __restrict__ out, int64_t n, T tau, const double* __restrict__ ss) {
+  // LpNorm.prox with proj_l2_ball (func/base.py:239-240, math/prox.py:207-210):
+  //   v = x/tau ; out = x - tau * (||v|| <= 1 ? v : (1*v)/||v||)
+  const T nv = (T)(sqrt(*ss) / (double)tau);
+  PCS_GRID_LOOP(p, n) {
+    const T v = x[p] / tau;
+    out[p] = x[p] - tau * ((nv <= T(1)) ? v : v / nv);
+  }
+}
+
+template <typename T>
+__global__ void k_prox_sql2(const T* __restrict__ x, T* __restrict__ out, int64_t n, T den) {
+  PCS_GRID_LOOP(p, n) out[p] = x[p] / den;
+}
+
+template <typename T>
+__global__ void k_proj_nonneg(const T* __restrict__ x, T* __restrict__ out, int64_t n) {
+  PCS_GRID_LOOP(p, n) {
+    const T v = x[p];
+    out[p] = (v < T(0)) ? T(0) : v;
+  }
+}
+
+template <typename T>
+__global__ void k_proj_segment(const T* __restrict__ x, T* __restrict__ out, int64_t n, T a, T b) {
+  PCS_GRID_LOOP(p, n) {
+    T v = x[p];
+    v = (v < a) ? a : v;
+    out[p] = (v > b) ? b : v;
+  }
+}
+
+template <typename T>
+__global__ void k_axpby(const T* __restrict__ x, const T* __restrict__ y, T* __restrict__ out, int64_t n, T a, T b) {
+  if (y) {
+    PCS_GRID_LOOP(p, n) out[p] = a * x[p] + b * y[p];
+  } else {
+    PCS_GRID_LOOP(p, n) out[p] = a * x[p];
+  }
+}
+
+template <typename T>
+__global__ void k_sub2(const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ w, T* __restrict__ out,
+                       int64_t n, T a, T b) {
+  PCS_GRID_LOOP(p, n) out[p] = (x[p] - a * y[p]) - b * w[p];
+}
+
+constexpr int kRedBlocks = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_reduce_stage1(int kind, const T* __restrict__ x, const T* __restrict__ y,
+                                                       int64_t n, double* __restrict__ part) {
+  __shared__ double sm[4];
+  double v[1] = {0.0};
+  PCS_GRID_LOOP(p, n) {
+    const double a = (double)x[p];
+    switch (kind) {
+      case 0: v[0] += a * a; break;
+      case 1: v[0] += fabs(a); break;
+      case 2: { const double dd = a - (double)y[p]; v[0] += dd * dd; } break;
+      default: v[0] += a * (double)y[p]; break;
+    }
+  }
+  block_sum<1>(v, sm);
+  if (threadIdx.x == 0) part[blockIdx.x] = v[0];
+}
+
+__global__ __launch_bounds__(256) void k_reduce_stage2(const double* __restrict__ part, int np,
+                                                       double* __restrict__ out) {
+  __shared__ double sm[4];
+  double v[1] = {0.0};
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v[0] += part[i];
+  block_sum<1>(v, sm);
+  if (threadIdx.x == 0) *out = v[0];
+}
+
+template <typename T>
+static int reduce(int kind, const void* x, const void* y, int64_t n, double* out, void* ws, hipStream_t st) {
+  if (!x || !out || !ws || n < 0 || kind < 0 || kind > 3 || (kind >= 2 && !y)) return PCS_EINVAL;
+  const unsigned g = grid_for(n, 256, kRedBlocks);
+  k_reduce_stage1<T><<<g, 256, 0, st>>>(kind, (const T*)x, (const T*)y, n, (double*)ws);
+  k_reduce_stage2<<<1, 256, 0, st>>>((const double*)ws, (int)g, out);
+  return launch_status();
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+#define PCS_DISPATCH(dt, ...)                            \
+  do {                                                   \
+    if ((dt) == PCS_F32) {                               \
+      using T = float;                                   \
+      __VA_ARGS__;                                       \
+    } else if ((dt) == PCS_F64) {                        \
+      using T = double;                                  \
+      __VA_ARGS__;                                       \
+    } else {                                             \
+      return PCS_EINVAL;                                 \
+    }                                                    \
+  } while (0)
+
+extern "C" {
+
+int pcs_prox_l1(int dt, const void* x, void* out, int64_t n, double tau, hipStream_t st) {
+  if (!x || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_prox_l1<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (T*)out, n, (T)tau));
+  return launch_status();
+}
+
+int pcs_fenchel_l1(int dt, const void* w, void* out, int64_t n, double sigma, double lam, hipStream_t st) {
+  if (!w || !out || n < 0) return PCS_EINVAL;
+  const double t = (1.0 / sigma) * lam;
+  PCS_DISPATCH(dt, k_fenchel_l1<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)w, (T*)out, n, (T)sigma, (T)t));
+  return launch_status();
+}
+
+int pcs_prox_l21_pixel(int dt, const void* x, void* out, int64_t npix, int d, double tau, hipStream_t st) {
+  if (!x || !out || npix < 0 || d < 1) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_prox_l21_pixel<T><<<grid_for(npix, 256), 256, 0, st>>>((const T*)x, (T*)out, npix, d, (T)tau));
+  return launch_status();
+}
+
+int pcs_fenchel_l21_pixel(int dt, const void* w, void* out, int64_t npix, int d, double sigma, double lam,
+                          hipStream_t st) {
+  if (!w || !out || npix < 0 || d < 1) return PCS_EINVAL;
+  const double t = (1.0 / sigma) * lam;
+  PCS_DISPATCH(dt, k_fenchel_l21_pixel<T><<<grid_for(npix, 256), 256, 0, st>>>((const T*)w, (T*)out, npix, d,
+                                                                                (T)sigma, (T)t));
+  return launch_status();
+}
+
+int pcs_prox_l21_labels(int dt, const void* x, void* out, int64_t n, const int32_t* gid, int64_t ngroups, double tau,
+                        void* ws, hipStream_t st) {
+  if (!x || !out || !gid || !ws || n < 0 || ngroups < 1) return PCS_EINVAL;
+  if (hipMemsetAsync(ws, 0, sizeof(double) * (size_t)ngroups, st) != hipSuccess) return PCS_ELAUNCH;
+  PCS_DISPATCH(dt, k_group_sumsq<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, gid, n, (double*)ws);
+               k_group_scale<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, gid, n, (const double*)ws, (T)tau,
+                                                                  (T*)out));
+  return launch_status();
+}
+
+int pcs_prox_l2(int dt, const void* x, void* out, int64_t n, double tau, const double* ss, hipStream_t st) {
+  if (!x || !out || !ss || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_prox_l2<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (T*)out, n, (T)tau, ss));
+  return launch_status();
+}
+
+int pcs_prox_sql2(int dt, const void* x, void* out, int64_t n, double tau, hipStream_t st) {
+  if (!x || !out || n < 0) return PCS_EINVAL;
+  const double den = 1.0 + 2.0 * tau;
+  PCS_DISPATCH(dt, k_prox_sql2<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (T*)out, n, (T)den));
+  return launch_status();
+}
+
+int pcs_proj_nonneg(int dt, const void* x, void* out, int64_t n, hipStream_t st) {
+  if (!x || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_proj_nonneg<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (T*)out, n));
+  return launch_status();
+}
+
+int pcs_proj_segment(int dt, const void* x, void* out, int64_t n, double a, double b, hipStream_t st) {
+  if (!x || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_proj_segment<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (T*)out, n, (T)a, (T)b));
+  return launch_status();
+}
+
+int pcs_axpby(int dt, const void* x, const void* y, void* out, int64_t n, double a, double b, hipStream_t st) {
+  if (!x || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_axpby<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (const T*)y, (T*)out, n, (T)a, (T)b));
+  return launch_status();
+}
+
+int pcs_sub2(int dt, const void* x, const void* y, const void* w, void* out, int64_t n, double a, double b,
+             hipStream_t st) {
+  if (!x || !y || !w || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_sub2<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (const T*)y, (const T*)w, (T*)out, n,
+                                                               (T)a, (T)b));
+  return launch_status();
+}
+
+int64_t pcs_reduce_ws_bytes(void) { return (int64_t)sizeof(double) * kRedBlocks; }
+
+int pcs_reduce(int dt, int kind, const void* x, const void* y, int64_t n, double* out, void* ws, hipStream_t st) {
+  if (dt == PCS_F32) return reduce<float>(kind, x, y, n, out, ws, st);
+  if (dt == PCS_F64) return reduce<double>(kind, x, y, n, out, ws, st);
+  return PCS_EINVAL;
+}
+
+}  // extern "C"

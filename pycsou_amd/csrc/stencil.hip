@@ -1,0 +1,234 @@
+// Finite-difference operators: FirstDerivative / Gradient / Laplacian.
+//
+// Replaces the PyLops 1.x arithmetic behind pycsou/linop/diff.py:128 (FirstDerivative),
+// :882 (Gradient = VStack of FirstDerivative) and :957 (Laplacian = w0*D2_0 + w1*D2_1).
+// Each output element is produced by one thread; neighbour loads are coalesced along
+// the contiguous axis and re-used through L1/L2.  The per-element operation order follows
+// the NumPy slicing order of PyLops 1.x so that fp64 results agree to the last ulp or two.
+#include "common.hpp"
+
+namespace pcs {
+
+struct Geo3 {
+  int64_t n[3];   // dims padded to 3 (leading 1s)
+  int64_t s[3];   // C-order strides
+  int64_t N;
+};
+
+static bool make_geo(int ndim, const int64_t* dims, Geo3& g) {
+  if (ndim < 1 || ndim > 3 || dims == nullptr) return false;
+  int pad = 3 - ndim;
+  for (int i = 0; i < 3; ++i) g.n[i] = (i < pad) ? 1 : dims[i - pad];
+  for (int i = 0; i < 3; ++i)
+    if (g.n[i] < 1) return false;
+  g.s[2] = 1;
+  g.s[1] = g.n[2];
+  g.s[0] = g.n[1] * g.n[2];
+  g.N = g.n[0] * g.n[1] * g.n[2];
+  return true;
+}
+
+__device__ __forceinline__ int64_t coord(const Geo3& g, int64_t p, int a) { return (p / g.s[a]) % g.n[a]; }
+
+// D_a x at p (pylops FirstDerivative._matvec_*)
+template <typename T>
+__device__ __forceinline__ T d1_fwd_at(const T* __restrict__ x, const Geo3& g, int64_t p, int a, T h, int kind,
+                                       int edge) {
+  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
+  if (kind == PCS_FORWARD) {
+    return (i < n - 1) ? (x[p + s] - x[p]) / h : T(0);
+  } else if (kind == PCS_BACKWARD) {
+    return (i > 0) ? (x[p] - x[p - s]) / h : T(0);
+  }
+  if (i > 0 && i < n - 1) return (T(0.5) * x[p + s] - T(0.5) * x[p - s]) / h;
+  if (!edge || n < 2) return T(0);
+  return (i == 0) ? (x[p + s] - x[p]) / h : (x[p] - x[p - s]) / h;
+}
+
+// (D_a^T y) at p (pylops FirstDerivative._rmatvec_*), accumulation order of the slicing code.
+template <typename T>
+__device__ __forceinline__ T d1_adj_at(const T* __restrict__ y, const Geo3& g, int64_t p, int a, T h, int kind,
+                                       int edge) {
+  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
+  T acc = T(0);
+  if (kind == PCS_FORWARD) {
+    if (i < n - 1) acc -= y[p] / h;
+    if (i > 0) acc += y[p - s] / h;
+  } else if (kind == PCS_BACKWARD) {
+    if (i < n - 1) acc -= y[p + s] / h;
+    if (i > 0) acc += y[p] / h;
+  } else {
+    if (i <= n - 3) acc -= (T(0.5) * y[p + s]) / h;
+    if (i >= 2) acc += (T(0.5) * y[p - s]) / h;
+    if (edge && n >= 2) {
+      if (i == 0) acc -= y[p] / h;
+      if (i == 1) acc += y[p - s] / h;
+      if (i == n - 2) acc -= y[p + s] / h;
+      if (i == n - 1) acc += y[p] / h;
+    }
+  }
+  return acc;
+}
+
+template <typename T>
+__global__ void k_deriv1_fwd(const T* __restrict__ x, T* __restrict__ out, Geo3 g, int a, T h, int kind, int edge) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x)
+    out[p] = d1_fwd_at(x, g, p, a, h, kind, edge);
+}
+
+template <typename T>
+__global__ void k_deriv1_adj(const T* __restrict__ y, T* __restrict__ out, Geo3 g, int a, T h, int kind, int edge) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x)
+    out[p] = d1_adj_at(y, g, p, a, h, kind, edge);
+}
+
+template <typename T>
+__global__ void k_grad_fwd(const T* __restrict__ x, T* __restrict__ out, Geo3 g, int nd, T h0, T h1, T h2, int kind,
+                           int edge) {
+  const T hs[3] = {h0, h1, h2};
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x) {
+    for (int k = 0; k < nd; ++k) out[k * g.N + p] = d1_fwd_at(x, g, p, 3 - nd + k, hs[k], kind, edge);
+  }
+}
+
+template <typename T>
+__global__ void k_grad_adj(const T* __restrict__ z, T* __restrict__ out, Geo3 g, int nd, T h0, T h1, T h2, int kind,
+                           int edge) {
+  const T hs[3] = {h0, h1, h2};
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x) {
+    T acc = T(0);
+    for (int k = 0; k < nd; ++k) acc += d1_adj_at(z + k * g.N, g, p, 3 - nd + k, hs[k], kind, edge);
+    out[p] = acc;
+  }
+}
+
+// SecondDerivative (pylops 1.x) along axis a at p.
+template <typename T>
+__device__ __forceinline__ T d2_fwd_at(const T* __restrict__ x, const Geo3& g, int64_t p, int a, T h2, int edge) {
+  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
+  if (i > 0 && i < n - 1) return (x[p + s] - T(2) * x[p] + x[p - s]) / h2;
+  if (!edge || n < 3) return T(0);
+  if (i == 0) return (x[p] - T(2) * x[p + s] + x[p + 2 * s]) / h2;
+  return (x[p - 2 * s] - T(2) * x[p - s] + x[p]) / h2;
+}
+
+template <typename T>
+__device__ __forceinline__ T d2_adj_at(const T* __restrict__ y, const Geo3& g, int64_t p, int a, T h2, int edge) {
+  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
+  T acc = T(0);
+  if (i <= n - 3) acc += y[p + s] / h2;
+  if (i >= 1 && i <= n - 2) acc -= (T(2) * y[p]) / h2;
+  if (i >= 2) acc += y[p - s] / h2;
+  if (edge && n >= 3) {
+    if (i == 0) acc += y[p] / h2;
+    if (i == 1) acc -= (T(2) * y[p - s]) / h2;
+    if (i == 2) acc += y[p - 2 * s] / h2;
+    if (i == n - 3) acc += y[p + 2 * s] / h2;
+    if (i == n - 2) acc -= (T(2) * y[p + s]) / h2;
+    if (i == n - 1) acc += y[p] / h2;
+  }
+  return acc;
+}
+
+template <typename T>
+__global__ void k_lap(const T* __restrict__ x, T* __restrict__ out, Geo3 g, T w0, T w1, T h20, T h21, int edge,
+                      int adj) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x) {
+    if (!adj)
+      out[p] = w0 * d2_fwd_at(x, g, p, 1, h20, edge) + w1 * d2_fwd_at(x, g, p, 2, h21, edge);
+    else
+      out[p] = w0 * d2_adj_at(x, g, p, 1, h20, edge) + w1 * d2_adj_at(x, g, p, 2, h21, edge);
+  }
+}
+
+template <typename T>
+static int deriv1(bool adj, const void* in, void* out, int ndim, const int64_t* dims, int axis, double step, int kind,
+                  int edge, hipStream_t st) {
+  Geo3 g;
+  if (!make_geo(ndim, dims, g) || axis < 0 || axis >= ndim || kind < 0 || kind > 2 || !in || !out)
+    return PCS_EINVAL;
+  const int a = 3 - ndim + axis;
+  const unsigned grid = grid_for(g.N, 256);
+  if (!adj)
+    k_deriv1_fwd<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, a, (T)step, kind, edge);
+  else
+    k_deriv1_adj<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, a, (T)step, kind, edge);
+  return launch_status();
+}
+
+template <typename T>
+static int grad(bool adj, const void* in, void* out, int ndim, const int64_t* dims, const double* steps, int kind,
+                int edge, hipStream_t st) {
+  Geo3 g;
+  if (!make_geo(ndim, dims, g) || kind < 0 || kind > 2 || !in || !out || !steps) return PCS_EINVAL;
+  const T h0 = (T)steps[0], h1 = ndim > 1 ? (T)steps[1] : T(1), h2 = ndim > 2 ? (T)steps[2] : T(1);
+  const unsigned grid = grid_for(g.N, 256);
+  if (!adj)
+    k_grad_fwd<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, ndim, h0, h1, h2, kind, edge);
+  else
+    k_grad_adj<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, ndim, h0, h1, h2, kind, edge);
+  return launch_status();
+}
+
+template <typename T>
+static int lap(bool adj, const void* in, void* out, const int64_t* dims, const double* w, const double* steps, int edge,
+               hipStream_t st) {
+  Geo3 g;
+  if (!make_geo(2, dims, g) || !in || !out || !w || !steps) return PCS_EINVAL;
+  const double h20 = steps[0] * steps[0], h21 = steps[1] * steps[1];
+  k_lap<T><<<grid_for(g.N, 256), 256, 0, st>>>((const T*)in, (T*)out, g, (T)w[0], (T)w[1], (T)h20, (T)h21, edge,
+                                               adj ? 1 : 0);
+  return launch_status();
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+extern "C" {
+
+int pcs_abi_version(void) { return 1; }
+
+int pcs_deriv1_fwd(int dt, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step, int kind,
+                   int edge, hipStream_t st) {
+  if (dt == PCS_F32) return deriv1<float>(false, x, out, ndim, dims, axis, step, kind, edge, st);
+  if (dt == PCS_F64) return deriv1<double>(false, x, out, ndim, dims, axis, step, kind, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_deriv1_adj(int dt, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step, int kind,
+                   int edge, hipStream_t st) {
+  if (dt == PCS_F32) return deriv1<float>(true, y, out, ndim, dims, axis, step, kind, edge, st);
+  if (dt == PCS_F64) return deriv1<double>(true, y, out, ndim, dims, axis, step, kind, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_grad_fwd(int dt, const void* x, void* out, int ndim, const int64_t* dims, const double* steps, int kind,
+                 int edge, hipStream_t st) {
+  if (dt == PCS_F32) return grad<float>(false, x, out, ndim, dims, steps, kind, edge, st);
+  if (dt == PCS_F64) return grad<double>(false, x, out, ndim, dims, steps, kind, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_grad_adj(int dt, const void* z, void* out, int ndim, const int64_t* dims, const double* steps, int kind,
+                 int edge, hipStream_t st) {
+  if (dt == PCS_F32) return grad<float>(true, z, out, ndim, dims, steps, kind, edge, st);
+  if (dt == PCS_F64) return grad<double>(true, z, out, ndim, dims, steps, kind, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_lap_fwd(int dt, const void* x, void* out, const int64_t* dims, const double* w, const double* steps, int edge,
+                hipStream_t st) {
+  if (dt == PCS_F32) return lap<float>(false, x, out, dims, w, steps, edge, st);
+  if (dt == PCS_F64) return lap<double>(false, x, out, dims, w, steps, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_lap_adj(int dt, const void* y, void* out, const int64_t* dims, const double* w, const double* steps, int edge,
+                hipStream_t st) {
+  if (dt == PCS_F32) return lap<float>(true, y, out, dims, w, steps, edge, st);
+  if (dt == PCS_F64) return lap<double>(true, y, out, dims, w, steps, edge, st);
+  return PCS_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,3 @@
+from .base import *  # noqa: F401,F403
+from .conv import *  # noqa: F401,F403
+from .diff import *  # noqa: F401,F403

@@ -1,0 +1,115 @@
+"""Convolution operators on the GPU (``pycsou/linop/conv.py`` hot-path subset).
+
+``Convolve2D(size, filter, shape)`` (``conv.py:167-295``) and
+``Convolve1D(size, filter, reshape_dims, axis)`` (``conv.py:20-164``) keep pycsou's
+offset rule (``K//2`` for odd, ``K//2 - 1`` for even filters, ``conv.py:159-162,
+285-292``) and PyLops 1.x semantics: forward = zero-boundary 'same' convolution,
+adjoint = correlation.  The reference goes through ``scipy.signal.convolve(method='fft')``;
+here both directions are direct LDS-tiled gfx950 kernels (``pcs_conv2d`` /
+``pcs_conv1d``), identical up to floating-point rounding.
+
+``Convolve2D.separable()`` exposes a rank-1 factorisation ``h = c r^T`` when the PSF has
+one (a Gaussian PSF does to ~1e-16): the fused PDS engine then applies the blur as two
+1-D passes inside its tile kernel (60 instead of 450 flop/pixel per direction).
+"""
+
+import numpy as np
+import torch
+
+from .. import _ops as O
+from ..core.linop import LinearOperator
+
+
+def pycsou_offset(n):
+    """``conv.py:159-162, 285-292``."""
+    return n // 2 - 1 if n % 2 == 0 else n // 2
+
+
+class _DevCache:
+    def __init__(self, arr):
+        self.arr = np.ascontiguousarray(arr)
+        self._d = {}
+
+    def get(self, dtype):
+        t = self._d.get(dtype)
+        if t is None:
+            t = torch.as_tensor(self.arr.reshape(-1)).to(device=O.device(), dtype=dtype).contiguous()
+            self._d[dtype] = t
+        return t
+
+
+class Convolve2DOp(LinearOperator):
+    def __init__(self, size, filter, shape, dtype='float64', method='fft'):
+        filt = np.asarray(filter, dtype=np.float64)
+        if filt.ndim != 2:
+            raise ValueError('filter must be a 2D array')
+        dims = tuple(int(s) for s in shape)
+        if len(dims) != 2 or dims[0] * dims[1] != size:
+            raise ValueError('shape and size are not compatible')
+        super().__init__(shape=(size, size), dtype=np.dtype(dtype), is_explicit=False, lipschitz_cst=np.inf)
+        self.filter, self.dims, self.method = filt, dims, method
+        self.kh, self.kw = filt.shape
+        self.off = (pycsou_offset(self.kh), pycsou_offset(self.kw))
+        self._h = _DevCache(filt)
+        self._hf = _DevCache(filt[::-1, ::-1])
+
+    def _apply(self, t):
+        return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off)
+
+    def _apply_minus(self, t, y):
+        """Conv x - y in one kernel (residual of the data-fidelity term)."""
+        return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off, b=y, beta=-1.0)
+
+    def _adj(self, t):
+        return O.conv2d(t, self.dims, self._hf.get(t.dtype), self.kh, self.kw, self.kh - 1 - self.off[0],
+                        self.kw - 1 - self.off[1])
+
+    def separable(self, rtol=1e-12):
+        """(taps_axis0, taps_axis1, half) with centred taps of length 2*half+1 if the PSF is
+        rank one to relative tolerance ``rtol``, else None."""
+        u, s, vt = np.linalg.svd(self.filter)
+        if s[0] == 0 or (s.size > 1 and s[1] > rtol * s[0]):
+            return None
+        c = u[:, 0] * np.sqrt(s[0])
+        r = vt[0] * np.sqrt(s[0])
+        if c.sum() < 0:
+            c, r = -c, -r
+        half = max(self.off[0], self.kh - 1 - self.off[0], self.off[1], self.kw - 1 - self.off[1])
+        t0 = np.zeros(2 * half + 1)
+        t1 = np.zeros(2 * half + 1)
+        # out[i] = sum_j h[j] x[i + off - j] = sum_s w[s] x[i - s], s = j - off  ->  w[s + half] = h[s + off]
+        t0[half - self.off[0]: half - self.off[0] + self.kh] = c
+        t1[half - self.off[1]: half - self.off[1] + self.kw] = r
+        return t0, t1, half
+
+
+def Convolve2D(size, filter, shape, dtype='float64', method='fft'):
+    """``pycsou/linop/conv.py:167-295``."""
+    return Convolve2DOp(size, filter, shape, dtype=dtype, method=method)
+
+
+class Convolve1DOp(LinearOperator):
+    def __init__(self, size, filter, reshape_dims=None, axis=0, dtype='float64', method=None):
+        h = np.asarray(filter, dtype=np.float64).reshape(-1)
+        dims = (size,) if reshape_dims is None else tuple(int(s) for s in reshape_dims)
+        if int(np.prod(dims)) != size:
+            raise ValueError('reshape_dims and size are not compatible')
+        if not 1 <= len(dims) <= 3:
+            raise NotImplementedError('Convolve1D supports 1-D to 3-D arrays')
+        super().__init__(shape=(size, size), dtype=np.dtype(dtype), is_explicit=False, lipschitz_cst=np.inf)
+        self.filter, self.dims, self.axis, self.method = h, dims, int(axis), method
+        self.k = h.size
+        self.off = pycsou_offset(self.k)
+        self._h = _DevCache(h)
+        self._hf = _DevCache(h[::-1])
+
+    def _apply(self, t):
+        return O.conv1d(t, self.dims, self.axis, self._h.get(t.dtype), self.k, self.off)
+
+    def _adj(self, t):
+        return O.conv1d(t, self.dims, self.axis, self._hf.get(t.dtype), self.k, self.k - 1 - self.off)
+
+
+def Convolve1D(size, filter, reshape_dims=None, axis=0, dtype='float64', method=None):
+    """``pycsou/linop/conv.py:20-164``."""
+    return Convolve1DOp(size, filter, reshape_dims=reshape_dims, axis=axis, dtype=dtype, method=method)

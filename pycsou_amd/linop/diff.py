@@ -1,0 +1,105 @@
+"""Finite-difference operators on the GPU (``pycsou/linop/diff.py`` hot-path subset).
+
+``FirstDerivative`` (``diff.py:24-130``), ``Gradient`` (``diff.py:777-882``) and
+``Laplacian`` (``diff.py:885-957``) keep the reference signatures and defaults and the
+PyLops 1.x arithmetic they delegate to (forward / backward / 3-point centred stencils,
+one-sided ends with ``edge=True``, ``Gradient`` = stacked ``[D_0 x; D_1 x; ...]``,
+adjoint = accumulated ``sum_k D_k^T z_k``).  Matvec and adjoint are the gfx950 kernels
+``pcs_deriv1_*``, ``pcs_grad_*``, ``pcs_lap_*``.
+"""
+
+from numbers import Number
+
+import numpy as np
+
+from .. import _ops as O
+from ..core.linop import LinearOperator
+
+
+def _steps(step, nd):
+    if isinstance(step, Number):
+        return [float(step)] * nd
+    step = [float(s) for s in step]
+    if len(step) != nd:
+        raise ValueError('step must be a float or one value per axis')
+    return step
+
+
+class _DiffOp(LinearOperator):
+    def __init__(self, shape, size, dtype):
+        super().__init__(shape=shape, dtype=np.dtype(dtype), is_explicit=False, lipschitz_cst=np.inf)
+        self._size = size
+
+
+class FirstDerivativeOp(_DiffOp):
+    """``pylops.FirstDerivative`` restated on the GPU."""
+
+    def __init__(self, size, shape=None, axis=0, step=1.0, edge=True, dtype='float64', kind='forward'):
+        if kind not in ('forward', 'centered', 'backward'):
+            raise NotImplementedError('kind must be forward, centered, or backward')
+        dims = (size,) if shape is None else tuple(int(s) for s in shape)
+        if int(np.prod(dims)) != size:
+            raise ValueError('shape and size are not compatible')
+        if not 1 <= len(dims) <= 3:
+            raise NotImplementedError('FirstDerivative supports 1-D to 3-D arrays')
+        super().__init__((size, size), size, dtype)
+        self.dims, self.axis, self.step, self.edge, self.kind = dims, int(axis), float(step), bool(edge), kind
+
+    def _apply(self, t):
+        return O.deriv1(t, self.dims, self.axis, self.step, self.kind, self.edge)
+
+    def _adj(self, t):
+        return O.deriv1(t, self.dims, self.axis, self.step, self.kind, self.edge, adjoint=True)
+
+
+def FirstDerivative(size, shape=None, axis=0, step=1.0, edge=True, dtype='float64', kind='forward'):
+    """``pycsou/linop/diff.py:24-130``."""
+    return FirstDerivativeOp(size, shape=shape, axis=axis, step=step, edge=edge, dtype=dtype, kind=kind)
+
+
+class GradientOp(_DiffOp):
+    """``pylops.Gradient`` = ``VStack([FirstDerivative(dir=k)])`` on the GPU."""
+
+    def __init__(self, shape, step=1.0, edge=True, dtype='float64', kind='centered'):
+        if kind not in ('forward', 'centered', 'backward'):
+            raise NotImplementedError('kind must be forward, centered, or backward')
+        dims = tuple(int(s) for s in shape)
+        if not 1 <= len(dims) <= 3:
+            raise NotImplementedError('Gradient supports 1-D to 3-D arrays')
+        N = int(np.prod(dims))
+        super().__init__((len(dims) * N, N), N, dtype)
+        self.dims, self.steps, self.edge, self.kind = dims, _steps(step, len(dims)), bool(edge), kind
+
+    def _apply(self, t):
+        return O.grad_fwd(t, self.dims, self.steps, self.kind, self.edge)
+
+    def _adj(self, t):
+        return O.grad_adj(t, self.dims, self.steps, self.kind, self.edge)
+
+
+def Gradient(shape, step=1., edge=True, dtype='float64', kind='centered'):
+    """``pycsou/linop/diff.py:777-882``."""
+    return GradientOp(shape, step=step, edge=edge, dtype=dtype, kind=kind)
+
+
+class LaplacianOp(_DiffOp):
+    """``pylops.Laplacian`` (2-D): ``w0 * D2_0 + w1 * D2_1`` on the GPU."""
+
+    def __init__(self, shape, weights=(1, 1), step=1., edge=True, dtype='float64'):
+        dims = tuple(int(s) for s in shape)
+        if len(dims) != 2:
+            raise NotImplementedError('Laplacian is 2-D in the reference (pycsou/linop/diff.py:885)')
+        N = int(np.prod(dims))
+        super().__init__((N, N), N, dtype)
+        self.dims, self.weights, self.steps, self.edge = dims, tuple(float(w) for w in weights), _steps(step, 2), bool(edge)
+
+    def _apply(self, t):
+        return O.lap(t, self.dims, self.weights, self.steps, self.edge)
+
+    def _adj(self, t):
+        return O.lap(t, self.dims, self.weights, self.steps, self.edge, adjoint=True)
+
+
+def Laplacian(shape, weights=(1, 1), step=1., edge=True, dtype='float64'):
+    """``pycsou/linop/diff.py:885-957``."""
+    return LaplacianOp(shape, weights=weights, step=step, edge=edge, dtype=dtype)

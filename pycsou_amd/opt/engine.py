@@ -1,0 +1,205 @@
+"""Fused, hipGraph-replayed PDS engine for 2-D TV problems (single GPU).
+
+Pattern-matches the problem a user script builds with the reference API
+(``F = (1/2)*SquaredL2Loss(dim, data=y) [* Convolve2D]``, ``K = Gradient(shape,
+kind='forward')``, ``H = lam * L21Norm(groups=tile(arange(N), 2))`` or ``lam * L1Norm``,
+``G = None / NonNegativeOrthant / Segment``) and runs ``PrimalDualSplitting.iterate``
+(``pycsou/opt/proxalgs.py:343-394`` inside ``pycsou/core/solver.py:55-76``) as
+
+    per iteration:  [GRADBUF only: r = h*x - y ; g = h^T r]   (pcs_conv2d x2)
+                    pcs_pds2d_step        x, z  ->  x', z', per-block norm partials
+                    pcs_pds_reduce_finalize      -> relative improvements, iteration
+                                                    counter, device stop flag
+
+captured once into a hipGraph of ``chunk`` iterations (x/z ping-pong between two
+buffers) and replayed.  The stop flag implements the reference loop condition on the
+device, so a replay after convergence is a sequence of no-op launches and the
+iteration count is exactly the reference's.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _lib as L
+from .. import _ops as O
+from ..core.functional import ProxFuncPostComp
+from ..core.map import DiffMapComp, DiffMapShifted
+from ..func.base import IndicatorFunctional, NullDifferentiableFunctional, NullProximableFunctional
+from ..func.penalty import L1Norm, L21Norm, SquaredL2Norm
+from ..linop.base import HomothetyMap
+from ..linop.conv import Convolve2DOp
+from ..linop.diff import GradientOp
+
+
+def _half_loss_data(F):
+    """If F is (1/2) * SquaredL2Norm.shifter(s) return s (the shift = -data), else None."""
+    if (isinstance(F, DiffMapComp) and isinstance(F.map1, HomothetyMap) and F.map1.cst == 0.5
+            and isinstance(F.map2, DiffMapShifted) and isinstance(F.map2.map, SquaredL2Norm)
+            and not np.isscalar(F.map2.shift)):
+        return F.map2.shift
+    return None
+
+
+def match_pds2d(F, G, H, K, has_H):
+    """Return an engine spec dict if (F, G, H, K) is a fused-engine problem, else None."""
+    if not has_H or not isinstance(K, GradientOp) or len(K.dims) != 2 or K.kind != 'forward':
+        return None
+    shape = K.dims
+    N = shape[0] * shape[1]
+    spec = {'shape': shape, 'steps': tuple(K.steps)}
+    # H = lam * (L1 | L21 pixel groups)
+    base, lam = H, 1.0
+    if isinstance(H, ProxFuncPostComp):
+        if H.shift != 0:
+            return None
+        base, lam = H.prox_func, float(H.scale)
+    if isinstance(base, L21Norm) and base.pixel_d == 2 and base.dim == 2 * N:
+        spec['hkind'] = L.PCS_H_L21
+    elif isinstance(base, L1Norm) and base.dim == 2 * N:
+        spec['hkind'] = L.PCS_H_L1
+    else:
+        return None
+    spec['lam'] = lam
+    # G
+    if G is None or isinstance(G, NullProximableFunctional):
+        spec['gkind'], spec['seg'] = L.PCS_G_NULL, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'nonneg':
+        spec['gkind'], spec['seg'] = L.PCS_G_NONNEG, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'segment':
+        spec['gkind'], spec['seg'] = L.PCS_G_SEGMENT, G.params
+    else:
+        return None
+    # F
+    if F is None or isinstance(F, NullDifferentiableFunctional):
+        spec['fkind'] = L.PCS_F_NULL
+        return spec
+    s = _half_loss_data(F)
+    if s is not None and O.numel(s) == N:
+        spec['fkind'], spec['shift'] = L.PCS_F_DENOISE, s
+        return spec
+    if isinstance(F, DiffMapComp) and isinstance(F.map2, Convolve2DOp) and F.map2.dims == shape:
+        s = _half_loss_data(F.map1)
+        if s is not None and O.numel(s) == N:
+            spec['fkind'], spec['shift'], spec['conv'] = L.PCS_F_SEPCONV, s, F.map2
+            return spec
+    return None
+
+
+class PDS2DEngine:
+    """Device state + captured loop for one fused 2-D PDS problem."""
+
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, chunk=32, use_graph=True):
+        self.lib = L.gpu()
+        self.spec = spec
+        self.dtype = dtype
+        n0, n1 = spec['shape']
+        self.N = n0 * n1
+        self.X = [x0.to(dtype).clone(), torch.empty(self.N, dtype=dtype, device=x0.device)]
+        self.Z = [z0.to(dtype).clone(), torch.empty(2 * self.N, dtype=dtype, device=x0.device)]
+        dev = self.X[0].device
+        self.chunk = max(2, chunk + (chunk % 2))
+        self.use_graph = use_graph
+        a = L.PdsArgs()
+        a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+        a.hkind, a.gkind = spec['hkind'], spec['gkind']
+        a.n0, a.n1, a.row0, a.rows = n0, n1, 0, n0
+        a.halo_x = a.halo_z = a.halo_y = 0
+        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+        a.step0, a.step1 = spec['steps']
+        a.seg_a, a.seg_b = spec['seg']
+        self.keep = []
+        fk = spec['fkind']
+        self.conv = None
+        if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV):
+            # y = -shift (exact), so x + shift == x - y bit for bit
+            self.y = -O.to_dev(spec['shift'], dtype)
+            a.y = self.y.data_ptr()
+        if fk == L.PCS_F_SEPCONV:
+            conv = spec['conv']
+            sep = conv.separable(rtol=2e-7 if dtype == torch.float32 else 1e-13)
+            if sep is not None:
+                t0, t1, half = sep
+                self.taps = [torch.as_tensor(t0).to(device=dev, dtype=dtype),
+                             torch.as_tensor(t1).to(device=dev, dtype=dtype)]
+                a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
+                a.half = half
+            else:
+                fk = L.PCS_F_GRADBUF
+                self.conv = conv
+                self.R = torch.empty(self.N, dtype=dtype, device=dev)
+                self.Gb = torch.empty(self.N, dtype=dtype, device=dev)
+                a.gbuf = self.Gb.data_ptr()
+        a.fkind = fk
+        self.fkind = fk
+        self.args = a
+        self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
+        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+        a.partials = self.partials.data_ptr()
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
+        a.ctrl = self.ctrl.data_ptr()
+        self.graph = None
+        self.hist = None
+        self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+
+    # one iteration with parity p (reads buffers p, writes 1-p)
+    def _iteration(self, p, hist):
+        a, lib, st = self.args, self.lib, L.stream()
+        if self.fkind == L.PCS_F_GRADBUF:
+            c = self.conv
+            h, hf = c._h.get(self.dtype), c._hf.get(self.dtype)
+            L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.X[p]), L.ptr(self.R), c.dims[0], c.dims[1], L.ptr(h), c.kh,
+                                   c.kw, c.off[0], c.off[1], L.ptr(self.y), -1.0, st), 'pcs_conv2d')
+            L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.R), L.ptr(self.Gb), c.dims[0], c.dims[1], L.ptr(hf), c.kh,
+                                   c.kw, c.kh - 1 - c.off[0], c.kw - 1 - c.off[1], None, 0.0, st), 'pcs_conv2d')
+        a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+        a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        L.check(lib.pcs_pds2d_step(ctypes.byref(a), st), 'pcs_pds2d_step')
+        L.check(lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl), L.ptr(hist), st),
+                'pcs_pds_reduce_finalize')
+
+    def _chunk(self, hist):
+        for i in range(self.chunk):
+            self._iteration(i % 2, hist)
+
+    def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        total = max(min_iter, max_iter) + 1
+        hist_len = 2 * total + 2
+        if self.hist is None or self.hist.numel() < hist_len:
+            # the history buffer is captured by pointer: (re)capture when it grows
+            self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
+            self.graph = None
+        hist = self.hist
+        hist.fill_(float('nan'))
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
+                                        int(has_dual), int(hist.numel()), L.stream()), 'pcs_ctrl_init2')
+        n_chunks = -(-total // self.chunk)
+        if self.use_graph:
+            if self.graph is None:
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._chunk(hist)
+                self.graph = g
+            pending = []
+            for k in range(n_chunks):
+                self.graph.replay()
+                ev = torch.cuda.Event()
+                self.ctrl_host.copy_(self.ctrl.view(torch.int32)[:2], non_blocking=True)
+                ev.record()
+                pending.append(ev)
+                if len(pending) >= 2:
+                    pending.pop(0).synchronize()
+                    if int(self.ctrl_host[1]) != 0:
+                        break
+        else:
+            for k in range(n_chunks):
+                self._chunk(hist)
+                if int(self.ctrl.view(torch.int32)[1].item()) != 0:
+                    break
+        torch.cuda.synchronize()
+        c = self.ctrl.view(torch.int32)[:2].cpu().numpy()
+        n = int(c[0])
+        h = hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
+        return n, self.X[n % 2], self.Z[n % 2], h

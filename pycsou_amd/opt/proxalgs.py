@@ -1,0 +1,432 @@
+"""Proximal algorithms (mirrors ``pycsou/opt/proxalgs.py``).
+
+Same classes, aliases, constructor signatures, validation errors, step-size and momentum
+rules, iterand dicts and diagnostics DataFrame as the reference:
+
+* ``PrimalDualSplitting`` / ``PDS`` (``proxalgs.py:27-394``)
+* ``AcceleratedProximalGradientDescent`` / ``APGD`` (``proxalgs.py:400-622``)
+* ``ChambollePockSplitting`` / ``CPS``, ``DouglasRachfordSplitting`` / ``DRS``,
+  ``ForwardBackwardSplitting`` / ``FBS`` (``proxalgs.py:628-862``)
+
+Execution: a PDS problem of the headline family (2-D TV denoising / deconvolution, see
+``opt/engine.py``) runs on the fused hipGraph engine; every other composition runs the
+reference iteration operator by operator on the GPU kernels (``update_iterand`` below),
+with the diagnostics norms reduced on the device.
+"""
+
+from numbers import Number
+
+import numpy as np
+import torch
+
+from .. import _ops as O
+from ..core.functional import ProximableFunctional
+from ..core.linop import LinearOperator
+from ..core.map import DifferentiableMap
+from ..core.solver import GenericIterativeAlgorithm
+from ..func.base import NullDifferentiableFunctional, NullProximableFunctional
+from ..linop.base import IdentityOperator, NullOperator
+
+
+def _frame(columns, rows):
+    from pandas import DataFrame
+    df = DataFrame(rows, columns=columns)
+    df['Iter'] = df['Iter'].astype(int)
+    return df
+
+
+def _find_arrays(obj, depth=0, out=None):
+    """Arrays (numpy / torch) referenced by a map tree (shifts, data): decides the output kind."""
+    out = [] if out is None else out
+    if depth > 8 or obj is None:
+        return out
+    for name in ('shift', 'data', 'mat'):
+        v = getattr(obj, name, None)
+        if isinstance(v, (np.ndarray, torch.Tensor)):
+            out.append(v)
+    for name in ('map', 'map1', 'map2', 'prox_func', 'Linop', 'LinOp1', 'LinOp2'):
+        _find_arrays(getattr(obj, name, None), depth + 1, out)
+    return out
+
+
+def _wants_torch(*objs):
+    for o in objs:
+        if isinstance(o, torch.Tensor):
+            return True
+    for o in objs:
+        for a in _find_arrays(o):
+            if isinstance(a, torch.Tensor):
+                return True
+    return False
+
+
+def _rel_improvement(old, new):
+    """||old - new|| / ||old|| (inf if ||old|| == 0), proxalgs.py:370-383."""
+    n_old = float(O.reduce_dev(0, old).item())
+    if n_old == 0:
+        return np.inf
+    return float(np.sqrt(O.reduce_dev(2, old, new).item()) / np.sqrt(n_old))
+
+
+class PrimalDualSplitting(GenericIterativeAlgorithm):
+    """Primal dual splitting (``pycsou/opt/proxalgs.py:27-394``)."""
+
+    def __init__(self, dim, F=None, G=None, H=None, K=None, tau=None, sigma=None, rho=None, beta=None, x0=None,
+                 z0=None, max_iter=500, min_iter=10, accuracy_threshold=1e-3, verbose=1, engine='auto'):
+        self.dim = dim
+        self._H = True
+        if isinstance(F, DifferentiableMap):
+            if F.shape[1] != dim:
+                raise ValueError(f'F does not have the proper dimension: {F.shape[1]}!={dim}.')
+            self.F = F
+            if F.diff_lipschitz_cst < np.inf:
+                self.beta = self.F.diff_lipschitz_cst if beta is None else beta
+            elif (beta is not None) and isinstance(beta, Number):
+                self.beta = beta
+            else:
+                raise ValueError('F must be a differentiable functional with Lipschitz-continuous gradient.')
+        elif F is None:
+            self.F = NullDifferentiableFunctional(dim=dim)
+            self.beta = 0
+        else:
+            raise TypeError(f'F must be of type {DifferentiableMap}.')
+
+        if isinstance(G, ProximableFunctional):
+            if G.dim != dim:
+                raise ValueError(f'G does not have the proper dimension: {G.dim}!={dim}.')
+            self.G = G
+        elif G is None:
+            self.G = NullProximableFunctional(dim=dim)
+        else:
+            raise TypeError(f'G must be of type {ProximableFunctional}.')
+
+        if isinstance(K, LinearOperator) and isinstance(H, ProximableFunctional):
+            if (K.shape[1] != dim) or (K.shape[0] != H.dim):
+                raise ValueError(f'Operator K with shape {K.shape} is inconsistent with functional H with dimension '
+                                 f'{H.dim}.')
+        if isinstance(H, ProximableFunctional):
+            self.H = H
+            if isinstance(K, LinearOperator):
+                self.K = K
+            elif K is None:
+                self.K = IdentityOperator(size=H.dim)
+                self.K.lipschitz_cst = self.K.diff_lipschitz_cst = 1
+            else:
+                raise TypeError(f'K must be of type {LinearOperator}.')
+        elif H is None:
+            self.H = NullProximableFunctional(dim=dim)
+            self._H = False
+            self.K = NullOperator(shape=(dim, dim))
+            self.K.lipschitz_cst = self.K.diff_lipschitz_cst = 0
+        else:
+            raise TypeError(f'H must be of type {ProximableFunctional}.')
+
+        if (tau is not None) and (sigma is not None):
+            self.tau, self.sigma = tau, sigma
+        elif (tau is not None) and (sigma is None):
+            self.tau = self.sigma = tau
+        elif (tau is None) and (sigma is not None):
+            self.tau = self.sigma = sigma
+        else:
+            self.tau, self.sigma = self.set_step_sizes()
+        self.rho = rho if rho is not None else self.set_momentum_term()
+
+        self._torch_out = _wants_torch(x0, z0, F)
+        self.x0 = x0 if x0 is not None else self.initialize_primal_variable()
+        self.z0 = z0 if z0 is not None else self.initialize_dual_variable()
+        self.engine_mode = engine
+        self._engine = None
+        objective_functional = (self.F + self.G) + (self.H * self.K)
+        init_iterand = {'primal_variable': self.x0, 'dual_variable': self.z0}
+        super().__init__(objective_functional=objective_functional, init_iterand=init_iterand, max_iter=max_iter,
+                         min_iter=min_iter, accuracy_threshold=accuracy_threshold, verbose=verbose)
+
+    # ---------------------------------------------------------------- reference rules
+    def set_step_sizes(self):
+        """``proxalgs.py:246-301``."""
+        if self.beta > 0:
+            if self._H is False:
+                return 2 / self.beta, 0
+            if self.K.lipschitz_cst < np.inf:
+                t = (1 / (self.K.lipschitz_cst) ** 2) * ((-self.beta / 4) + np.sqrt((self.beta ** 2 / 16)
+                                                                                    + self.K.lipschitz_cst ** 2))
+                return t, t
+        else:
+            if self._H is False:
+                return 1, 0
+            if self.K.lipschitz_cst < np.inf:
+                return 1 / self.K.lipschitz_cst, 1 / self.K.lipschitz_cst
+        raise ValueError('Please compute the Lipschitz constant of the linear operator K by calling its method '
+                         '"compute_lipschitz_cst()".')
+
+    def set_momentum_term(self):
+        """``proxalgs.py:303-316``."""
+        return 0.9 if self.beta > 0 else 1
+
+    def initialize_primal_variable(self):
+        return np.zeros(shape=(self.dim,), dtype=np.float64)
+
+    def initialize_dual_variable(self):
+        if self._H is False:
+            return None
+        return np.zeros(shape=(self.H.dim,), dtype=np.float64)
+
+    # ---------------------------------------------------------------- dtype / kind
+    def _compute_dtype(self):
+        for a in [self.x0] + _find_arrays(self.F):
+            if isinstance(a, torch.Tensor) and a.dtype in (torch.float32, torch.float64):
+                return a.dtype
+            if isinstance(a, np.ndarray) and a.dtype in (np.float32, np.float64):
+                return torch.float32 if a.dtype == np.float32 else torch.float64
+        return torch.float64
+
+    def _out(self, t):
+        if t is None:
+            return None
+        return t if self._torch_out else t.detach().cpu().numpy()
+
+    # ---------------------------------------------------------------- fused engine
+    def _fused_spec(self):
+        if self.engine_mode in (False, 'generic'):
+            return None
+        from .engine import match_pds2d
+        return match_pds2d(None if isinstance(self.F, NullDifferentiableFunctional) else self.F, self.G, self.H,
+                           self.K, self._H)
+
+    def iterate(self):
+        spec = self._fused_spec()
+        if spec is None:
+            if self.engine_mode == 'fused':
+                raise ValueError('problem does not match the fused PDS engine')
+            return self._iterate_generic()
+        from .engine import PDS2DEngine
+        dtype = self._compute_dtype()
+        x0 = O.to_dev(self.x0, dtype)
+        z0 = O.to_dev(self.z0, dtype)
+        self._engine = PDS2DEngine(spec, dtype, self.tau, self.sigma, self.rho, x0, z0)
+        n, x, z, hist = self._engine.run(self.max_iter, self.min_iter, self.accuracy_threshold, has_dual=True)
+        self.iter = n
+        rows = [[i, hist[i, 0], hist[i, 1]] for i in range(n)]
+        self.diagnostics = _frame(['Iter', 'Relative Improvement (primal variable)',
+                                   'Relative Improvement (dual variable)'], rows)
+        self.converged = True
+        self.iterand = {'primal_variable': self._out(x), 'dual_variable': self._out(z)}
+        return self.iterand, self.converged, self.diagnostics
+
+    # ---------------------------------------------------------------- generic device path
+    def _iterate_generic(self):
+        dtype = self._compute_dtype()
+        self._state = {'primal_variable': O.to_dev(self.x0, dtype),
+                       'dual_variable': None if self.z0 is None else O.to_dev(self.z0, dtype)}
+        self._old = dict(self._state)
+        self._rows = []
+        self.init_iterand_dev = dict(self._state)
+        while ((self.iter <= self.max_iter) and (self.stopping_metric() > self.accuracy_threshold)) or (
+                self.iter <= self.min_iter):
+            self._state = self._update_dev(self._state)
+            self.update_diagnostics()
+            if self.verbose is not None and self.iter % self.verbose == 0:
+                self.print_diagnostics()
+            self._old = self._state
+            self.iter += 1
+        self.converged = True
+        cols = ['Iter', 'Relative Improvement (primal variable)']
+        if self._H:
+            cols.append('Relative Improvement (dual variable)')
+        self.diagnostics = _frame(cols, self._rows)
+        self.iterand = {'primal_variable': self._out(self._state['primal_variable']),
+                        'dual_variable': self._out(self._state['dual_variable'])}
+        return self.iterand, self.converged, self.diagnostics
+
+    def _update_dev(self, st):
+        """``PrimalDualSplitting.update_iterand`` (proxalgs.py:343-355) on device tensors."""
+        x, z = st['primal_variable'], st['dual_variable']
+        g = self.F._grad(x)
+        if self._H:
+            v = O.sub2(x, g, self.K._adj(z), self.tau, self.tau)
+        else:
+            v = O.axpby(x, g, 1.0, -self.tau)
+        x_temp = self.G._prox(v, self.tau)
+        if self._H:
+            u = O.axpby(x_temp, x, 2.0, -1.0)
+            w = O.axpby(z, self.K._apply(u), 1.0, self.sigma)
+            z_temp = self.H._fenchel(w, self.sigma)
+            z = O.axpby(z_temp, z, self.rho, 1 - self.rho)
+        x = O.axpby(x_temp, x, self.rho, 1 - self.rho)
+        return {'primal_variable': x, 'dual_variable': z}
+
+    def update_iterand(self):
+        if not hasattr(self, '_state') or self.iter == 0:
+            dtype = self._compute_dtype()
+            self._state = {'primal_variable': O.to_dev(self.x0, dtype),
+                           'dual_variable': None if self.z0 is None else O.to_dev(self.z0, dtype)}
+        self._state = self._update_dev(self._state)
+        return {'primal_variable': self._out(self._state['primal_variable']),
+                'dual_variable': self._out(self._state['dual_variable'])}
+
+    def print_diagnostics(self):
+        print(dict(zip(['Iter', 'Relative Improvement (primal variable)', 'Relative Improvement (dual variable)'],
+                       self._rows[-1])))
+
+    def stopping_metric(self):
+        if self.iter == 0:
+            return np.inf
+        return self._rows[self.iter - 1][1]
+
+    def update_diagnostics(self):
+        row = [self.iter, _rel_improvement(self._old['primal_variable'], self._state['primal_variable'])]
+        if self._H:
+            row.append(_rel_improvement(self._old['dual_variable'], self._state['dual_variable']))
+        self._rows.append(row)
+
+
+PDS = PrimalDualSplitting
+
+
+class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
+    """Accelerated proximal gradient descent (``pycsou/opt/proxalgs.py:400-622``)."""
+
+    def __init__(self, dim, F=None, G=None, tau=None, acceleration='CD', beta=None, x0=None, max_iter=500,
+                 min_iter=10, accuracy_threshold=1e-3, verbose=1, d=75.):
+        self.dim = dim
+        self.acceleration = acceleration
+        self.d = d
+        if isinstance(F, DifferentiableMap):
+            if F.shape[1] != dim:
+                raise ValueError(f'F does not have the proper dimension: {F.shape[1]}!={dim}.')
+            self.F = F
+            if F.diff_lipschitz_cst < np.inf:
+                self.beta = self.F.diff_lipschitz_cst if beta is None else beta
+            elif (beta is not None) and isinstance(beta, Number):
+                self.beta = beta
+            else:
+                raise ValueError('F must be a differentiable functional with Lipschitz-continuous gradient.')
+        elif F is None:
+            self.F = NullDifferentiableFunctional(dim=dim)
+            self.beta = 0
+        else:
+            raise TypeError(f'F must be of type {DifferentiableMap}.')
+        if isinstance(G, ProximableFunctional):
+            if G.dim != dim:
+                raise ValueError(f'G does not have the proper dimension: {G.dim}!={dim}.')
+            self.G = G
+        elif G is None:
+            self.G = NullProximableFunctional(dim=dim)
+        else:
+            raise TypeError(f'G must be of type {ProximableFunctional}.')
+        self.tau = tau if tau is not None else self.set_step_size()
+        self._torch_out = _wants_torch(x0, F)
+        self.x0 = x0 if x0 is not None else self.initialize_iterate()
+        objective_functional = self.F + self.G
+        init_iterand = {'iterand': self.x0, 'past_aux': 0 * self.x0, 'past_t': 1}
+        super().__init__(objective_functional=objective_functional, init_iterand=init_iterand, max_iter=max_iter,
+                         min_iter=min_iter, accuracy_threshold=accuracy_threshold, verbose=verbose)
+
+    def set_step_size(self):
+        return 1 / self.beta
+
+    def initialize_iterate(self):
+        return np.zeros(shape=(self.dim,), dtype=np.float64)
+
+    def _compute_dtype(self):
+        for a in [self.x0] + _find_arrays(self.F):
+            if isinstance(a, torch.Tensor) and a.dtype in (torch.float32, torch.float64):
+                return a.dtype
+            if isinstance(a, np.ndarray) and a.dtype in (np.float32, np.float64):
+                return torch.float32 if a.dtype == np.float32 else torch.float64
+        return torch.float64
+
+    def _out(self, t):
+        return t if self._torch_out else t.detach().cpu().numpy()
+
+    def iterate(self):
+        dtype = self._compute_dtype()
+        x0 = O.to_dev(self.x0, dtype)
+        self._state = (x0, torch.zeros_like(x0), 1)
+        self._old = x0
+        self._rows = []
+        while ((self.iter <= self.max_iter) and (self.stopping_metric() > self.accuracy_threshold)) or (
+                self.iter <= self.min_iter):
+            self._state = self._update_dev(self._state)
+            self.update_diagnostics()
+            if self.verbose is not None and self.iter % self.verbose == 0:
+                self.print_diagnostics()
+            self._old = self._state[0]
+            self.iter += 1
+        self.converged = True
+        self.diagnostics = _frame(['Iter', 'Relative Improvement'], self._rows)
+        x, aux, t = self._state
+        self.iterand = {'iterand': self._out(x), 'past_aux': self._out(aux), 'past_t': t}
+        return self.iterand, self.converged, self.diagnostics
+
+    def _update_dev(self, st):
+        """``proxalgs.py:586-601``."""
+        x, x_old, t_old = st
+        x_temp = self.G._prox(O.axpby(x, self.F._grad(x), 1.0, -self.tau), self.tau)
+        if self.acceleration == 'BT':
+            t = (1 + np.sqrt(1 + 4 * t_old ** 2)) / 2
+        elif self.acceleration == 'CD':
+            t = (self.iter + self.d) / self.d
+        else:
+            t = t_old = 1
+        a = (t_old - 1) / t
+        x = O.axpby(x_temp, O.axpby(x_temp, x_old, 1.0, -1.0), 1.0, a)
+        return (x, x_temp, t)
+
+    def update_iterand(self):
+        if not hasattr(self, '_state') or self.iter == 0:
+            x0 = O.to_dev(self.x0, self._compute_dtype())
+            self._state = (x0, torch.zeros_like(x0), 1)
+        self._state = self._update_dev(self._state)
+        x, aux, t = self._state
+        return {'iterand': self._out(x), 'past_aux': self._out(aux), 'past_t': t}
+
+    def print_diagnostics(self):
+        print(dict(zip(['Iter', 'Relative Improvement'], self._rows[-1])))
+
+    def stopping_metric(self):
+        if self.iter == 0:
+            return np.inf
+        return self._rows[self.iter - 1][1]
+
+    def update_diagnostics(self):
+        self._rows.append([self.iter, _rel_improvement(self._old, self._state[0])])
+
+
+APGD = AcceleratedProximalGradientDescent
+
+
+class ChambollePockSplitting(PrimalDualSplitting):
+    """``proxalgs.py:628-716``: PDS with F = 0, rho = 1."""
+
+    def __init__(self, dim, G=None, H=None, K=None, tau=None, sigma=None, rho=1, x0=None, z0=None, max_iter=500,
+                 min_iter=10, accuracy_threshold=1e-3, verbose=1):
+        super().__init__(dim=dim, F=None, G=G, H=H, K=K, tau=tau, sigma=sigma, rho=rho, x0=x0, z0=z0,
+                         max_iter=max_iter, min_iter=min_iter, accuracy_threshold=accuracy_threshold, verbose=verbose)
+
+
+CPS = ChambollePockSplitting
+
+
+class DouglasRachfordSplitting(PrimalDualSplitting):
+    """``proxalgs.py:719-781``: PDS with F = 0, K = I, sigma = 1/tau, rho = 1."""
+
+    def __init__(self, dim, G=None, H=None, tau=1., x0=None, z0=None, max_iter=500, min_iter=10,
+                 accuracy_threshold=1e-3, verbose=1):
+        super().__init__(dim=dim, F=None, G=G, H=H, K=None, tau=tau, sigma=1 / tau, rho=1, x0=x0, z0=z0,
+                         max_iter=max_iter, min_iter=min_iter, accuracy_threshold=accuracy_threshold, verbose=verbose)
+
+
+DRS = DouglasRachfordSplitting
+
+
+class ForwardBackwardSplitting(PrimalDualSplitting):
+    """``proxalgs.py:784-862``: PDS with H = 0."""
+
+    def __init__(self, dim, F=None, G=None, tau=None, rho=1, x0=None, max_iter=500, min_iter=10,
+                 accuracy_threshold=1e-3, verbose=1):
+        super().__init__(dim=dim, F=F, G=G, H=None, K=None, tau=tau, rho=rho, x0=x0, max_iter=max_iter,
+                         min_iter=min_iter, accuracy_threshold=accuracy_threshold, verbose=verbose)
+
+
+FBS = ForwardBackwardSplitting

@@ -1,0 +1,247 @@
+"""HIP kernels vs the oracle, operator by operator (through the C ABI).
+
+Tolerances: fp64 kernels agree with the NumPy/SciPy oracle to <= 1e-12 relative (direct
+convolution vs the reference's FFT path, FMA contraction); fp32 kernels to <= 2e-6
+relative (single rounding per op).  Prox / projection kernels are compared
+element-wise.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pylops1 as P
+from oracle import pycsou_ref as OR
+from tests.cases import load, rel
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.float64: 1e-12, np.float32: 2e-6}
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope='module')
+def A():
+    import pycsou_amd as pa
+    from pycsou_amd import _ops
+    return pa, _ops
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('shape', [(64, 64), (63, 65), (1, 17), (5, 6, 7), (16, 17, 18), (129,)])
+@pytest.mark.parametrize('kind', ['forward', 'backward', 'centered'])
+@pytest.mark.parametrize('edge', [True, False])
+def test_gradient(A, dtype, shape, kind, edge):
+    from pycsou_amd.linop.diff import Gradient
+    rng = np.random.default_rng(0)
+    steps = [1.0 + 0.25 * i for i in range(len(shape))]
+    x = rng.standard_normal(int(np.prod(shape))).astype(dtype)
+    ref = P.Gradient(shape, sampling=steps, edge=edge, kind=kind, dtype=np.float64)
+    op = Gradient(shape, step=steps, edge=edge, kind=kind)
+    y = op(x)
+    assert y.dtype == dtype
+    assert rel(y, ref.matvec(x.astype(np.float64))) < TOL[dtype]
+    z = rng.standard_normal(op.shape[0]).astype(dtype)
+    assert rel(op.adjoint(z), ref.rmatvec(z.astype(np.float64))) < TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('axis', [0, 1, 2])
+def test_first_derivative(A, dtype, axis):
+    from pycsou_amd.linop.diff import FirstDerivative
+    shape = (9, 10, 11)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(990).astype(dtype)
+    for kind in ['forward', 'backward', 'centered']:
+        ref = P.FirstDerivative(990, dims=shape, dir=axis, sampling=0.5, edge=True, kind=kind)
+        op = FirstDerivative(990, shape=shape, axis=axis, step=0.5, kind=kind)
+        assert rel(op(x), ref.matvec(x.astype(np.float64))) < TOL[dtype]
+        assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < TOL[dtype]
+
+
+def test_first_derivative_doctest(A):
+    from pycsou_amd.linop.diff import FirstDerivative
+    f = load('ops.npz')
+    x = f['doc_d1_x']
+    y = FirstDerivative(size=x.size) * x
+    assert np.sum(np.abs(y) > 0) == 6
+    np.testing.assert_allclose(y, f['doc_d1_y'])
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('edge', [True, False])
+def test_laplacian(A, dtype, edge):
+    from pycsou_amd.linop.diff import Laplacian
+    shape = (37, 45)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal(37 * 45).astype(dtype)
+    ref = P.Laplacian(shape, weights=(1.0, 0.5), sampling=(1.0, 2.0), edge=edge)
+    op = Laplacian(shape, weights=(1.0, 0.5), step=(1.0, 2.0), edge=edge)
+    assert rel(op(x), ref.matvec(x.astype(np.float64))) < TOL[dtype]
+    assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('kshape', [(15, 15), (4, 6), (7, 4), (1, 5), (9, 1), (31, 31), (40, 3)])
+@pytest.mark.parametrize('shape', [(64, 64), (70, 33), (5, 200)])
+def test_convolve2d(A, dtype, kshape, shape):
+    from pycsou_amd.linop.conv import Convolve2D
+    rng = np.random.default_rng(3)
+    h = rng.standard_normal(kshape)
+    N = shape[0] * shape[1]
+    x = rng.standard_normal(N).astype(dtype)
+    off = tuple(P.pycsou_offset(n) for n in kshape)
+    ref = P.Convolve2D(N, h, shape, offset=off, method='direct')
+    op = Convolve2D(N, h, shape)
+    assert rel(op(x), ref.matvec(x.astype(np.float64))) < 10 * TOL[dtype]
+    assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
+
+
+def test_convolve2d_doctest(A):
+    from pycsou_amd.linop.conv import Convolve2D
+    f = load('ops.npz')
+    op = Convolve2D(size=10000, filter=f['doc_conv2d_h'], shape=(100, 100))
+    np.testing.assert_allclose(op * f['doc_conv2d_x'], f['doc_conv2d_y'], atol=1e-12)
+
+
+def test_convolve1d_doctest(A):
+    from pycsou_amd.linop.conv import Convolve1D
+    f = load('ops.npz')
+    op = Convolve1D(size=30, filter=f['doc_conv1d_h'])
+    np.testing.assert_allclose(op * f['doc_conv1d_x'], f['doc_conv1d_y'], atol=1e-14)
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('axis', [0, 1, 2])
+@pytest.mark.parametrize('k', [15, 4, 1])
+def test_convolve1d_axis(A, dtype, axis, k):
+    from pycsou_amd.linop.conv import Convolve1D
+    dims = (12, 13, 14)
+    N = int(np.prod(dims))
+    rng = np.random.default_rng(4)
+    h = rng.standard_normal(k)
+    x = rng.standard_normal(N).astype(dtype)
+    ref = P.Convolve1D(N, h, offset=P.pycsou_offset(k), dims=dims, dir=axis)
+    op = Convolve1D(N, h, reshape_dims=dims, axis=axis)
+    assert rel(op(x), ref.matvec(x.astype(np.float64))) < 10 * TOL[dtype]
+    assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
+
+
+def test_separable_factorisation(A):
+    from pycsou_amd.linop.conv import Convolve2D
+    for (kh, kw) in [(15, 15), (4, 6), (7, 3)]:
+        c = np.exp(-np.linspace(-2, 2, kh) ** 2)
+        r = np.exp(-np.linspace(-1, 1.5, kw) ** 2)
+        op = Convolve2D(64 * 64, np.outer(c, r), (64, 64))
+        t0, t1, half = op.separable()
+        # rebuild the centred filter and compare to the PSF placed by its offsets
+        full = np.outer(t0, t1)
+        o0, o1 = op.off
+        np.testing.assert_allclose(full[half - o0:half - o0 + kh, half - o1:half - o1 + kw], op.filter, atol=1e-14)
+        assert abs(full.sum() - op.filter.sum()) < 1e-12
+    assert Convolve2D(64 * 64, np.random.default_rng(0).standard_normal((5, 5)), (64, 64)).separable() is None
+
+
+# ---------------------------------------------------------------- prox / functionals vs reference fixtures
+
+def test_prox_vs_reference_fixtures(A):
+    from pycsou_amd.func.penalty import L1Norm, L2Norm, L21Norm, SquaredL2Norm, NonNegativeOrthant, Segment
+    f = load('prox.npz')
+    x, vz, groups = f['x'], f['vz'], f['groups']
+    np.testing.assert_allclose(L1Norm(200).prox(x, 0.7), f['l1_prox_07'], atol=1e-15)
+    np.testing.assert_allclose(L1Norm(200)(x), f['l1_value'], rtol=1e-14)
+    np.testing.assert_allclose(L2Norm(200).prox(x, 3.0), f['l2_prox_3'], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(L2Norm(200).prox(x, 30.0), f['l2_prox_30'], atol=1e-15)
+    l21 = L21Norm(dim=200, groups=groups)
+    np.testing.assert_allclose(l21.prox(x, 0.5), f['l21_prox_05'], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(l21(x), f['l21_value'], rtol=1e-13)
+    l21p = L21Norm(dim=200, groups=np.tile(np.arange(100), 2))
+    assert l21p.pixel_d == 2
+    np.testing.assert_allclose(l21p.prox(vz, 0.5), f['l21pix_prox_05'], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(l21p(vz), f['l21pix_value'], rtol=1e-13)
+    np.testing.assert_allclose((0.3 * L1Norm(200)).fenchel_prox(x, 0.7), f['fenchel_l1_lam03_s07'], atol=1e-15)
+    np.testing.assert_allclose((0.3 * l21p).fenchel_prox(vz, 0.7), f['fenchel_l21pix_lam03_s07'], rtol=1e-13,
+                               atol=1e-15)
+    np.testing.assert_allclose(SquaredL2Norm(200)(x), f['sql2_value'], rtol=1e-13)
+    np.testing.assert_array_equal(SquaredL2Norm(200).gradient(x), f['sql2_grad'])
+    np.testing.assert_array_equal(NonNegativeOrthant(200).prox(x, 1.0), f['nonneg'])
+    np.testing.assert_array_equal(Segment(200, a=-0.5, b=0.25).prox(x, 1.0), f['segment'])
+    np.testing.assert_allclose(SquaredL2Norm(200).prox(x, 0.25), x / 1.5, rtol=1e-15)
+
+
+def test_reference_doctests(A):
+    from pycsou_amd.func.penalty import L1Norm, L2Norm, L21Norm, SquaredL2Norm
+    from pycsou_amd.math.prox import soft
+    x = np.arange(10, dtype=np.float64)
+    assert L1Norm(10)(x) == 45.0
+    assert abs(L2Norm(10)(x) - 16.881943016134134) < 1e-14
+    assert abs(L21Norm(10, groups=np.concatenate((np.ones(5), 2 * np.ones(5))))(x) - 21.44594499772297) < 1e-13
+    assert abs(SquaredL2Norm(10)(x) - 285.00000000000006) < 1e-12
+    np.testing.assert_array_equal(soft(np.linspace(-1, 1, 5), 0.5), [-0.5, -0., 0., 0., 0.5])
+    # prox calculus identities (pycsou/core/functional.py:122-132)
+    f = L1Norm(10)
+    np.testing.assert_allclose((2 * f).prox(x, 0.1), f.prox(x, 0.2))
+    np.testing.assert_allclose((f * 2).prox(x, 0.1), f.prox(2 * x, 0.4) / 2)
+    np.testing.assert_allclose(f.shifter(x).prox(x, 0.1), f.prox(x + x, 0.1) - x)
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+def test_prox_large_fp32(A, dtype):
+    from pycsou_amd import _ops
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    x = rng.standard_normal(2 * n).astype(dtype)
+    t = dev(x)
+    np.testing.assert_allclose(host(_ops.prox_l1(t, 0.3)), OR.prox_l1(x.copy(), dtype(0.3)), rtol=0,
+                               atol=4 * np.finfo(dtype).eps)
+    got = host(_ops.fenchel_l21_pixel(t, 0.7, 0.2, 2))
+    want = OR.fenchel_prox(OR.postcomp(lambda v, s: OR.prox_l21_pixel(v, s, 2), 0.2), x.astype(np.float64), 0.7)
+    assert rel(got, want) < TOL[dtype]
+
+
+def test_reductions(A):
+    from pycsou_amd import _ops
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal(3_000_001)
+    y = rng.standard_normal(3_000_001)
+    tx, ty = dev(x), dev(y)
+    assert abs(_ops.reduce_dev(0, tx).item() - np.dot(x, x)) < 1e-9 * np.dot(x, x)
+    assert abs(_ops.reduce_dev(1, tx).item() - np.abs(x).sum()) < 1e-9 * np.abs(x).sum()
+    assert abs(_ops.reduce_dev(2, tx, ty).item() - np.sum((x - y) ** 2)) < 1e-9 * np.sum((x - y) ** 2)
+    assert abs(_ops.reduce_dev(3, tx, ty).item() - np.dot(x, y)) < 1e-8 * np.sqrt(np.dot(x, x) * np.dot(y, y))
+    # deterministic: same bits twice
+    assert _ops.reduce_dev(0, tx).item() == _ops.reduce_dev(0, tx).item()
+    assert _ops.reduce_dev(0, dev(np.zeros(0))).item() == 0.0
+
+
+def test_abi_errors(A):
+    from pycsou_amd import _lib as L
+    lib = L.gpu()
+    t = torch.zeros(16, device='cuda')
+    assert lib.pcs_grad_fwd(7, L.ptr(t), L.ptr(t), 2, L.i64s([4, 4]), L.dbls([1, 1]), 0, 1, L.stream()) == -1
+    assert lib.pcs_grad_fwd(0, L.ptr(t), L.ptr(t), 4, L.i64s([1, 1, 4, 4]), L.dbls([1] * 4), 0, 1, L.stream()) == -1
+    assert lib.pcs_conv2d(0, L.ptr(t), L.ptr(t), 4, 4, L.ptr(t), 3, 3, 3, 1, None, 0.0, L.stream()) == -1
+    with pytest.raises(L.HipError):
+        L.check(lib.pcs_prox_l1(0, None, L.ptr(t), 16, 1.0, L.stream()), 'pcs_prox_l1')
+
+
+def test_lipschitz_lanczos(A):
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.linop.conv import Convolve2D
+    G = Gradient((32, 40), kind='forward')
+    G.compute_lipschitz_cst()
+    # ||grad_fwd||^2 on a grid = 4 sin^2(pi (n0-1)/(2 n0)) + 4 sin^2(pi (n1-1)/(2 n1))
+    exact = np.sqrt(4 * np.sin(np.pi * 31 / 64) ** 2 + 4 * np.sin(np.pi * 39 / 80) ** 2)
+    assert abs(G.lipschitz_cst - exact) < 1e-6 * exact
+    h = OR.gaussian_psf(7, 1.5)
+    C = Convolve2D(64 * 64, h, (64, 64))
+    C.compute_lipschitz_cst()
+    dense = np.stack([P.Convolve2D(4096, h, (64, 64), offset=(3, 3)).matvec(e) for e in np.eye(4096)[:: 1]]).T
+    assert abs(C.lipschitz_cst - np.linalg.norm(dense, 2)) < 1e-6

@@ -1,0 +1,105 @@
+"""CPU-side tests: the C-ABI library loads and exports the declared symbols, and the host
+logic (algebra, Lipschitz propagation, step sizes, dispatch, validation) matches the
+reference.  No compute calls (no GPU here)."""
+
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.cases import pds_case, pds_case_names
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    hdr = open(os.path.join(REPO, 'include', 'pycsou_hip.h')).read()
+    declared = set(re.findall(r'^\s*(?:int|int64_t)\s+(pcs_\w+)\(', hdr, flags=re.M))
+    assert len(declared) >= 25
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared <= set(_lib.EXPORTS), declared - set(_lib.EXPORTS)
+    assert lib.pcs_abi_version() == 1
+    assert lib.pcs_ctrl_bytes() == 64
+    assert lib.pcs_pds2d_halo_x(7) == 15
+
+
+def test_compute_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from pycsou_amd.func.penalty import L1Norm
+    with pytest.raises(RuntimeError, match='no ROCm GPU'):
+        L1Norm(4).prox(np.ones(4), 0.1)
+
+
+def test_lipschitz_propagation_and_types():
+    from pycsou_amd.core.map import DiffMapComp
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L1Norm, L21Norm, L2Norm, SquaredL2Norm
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.base import HomothetyMap
+    N = 16
+    half = (1 / 2) * SquaredL2Loss(dim=N, data=np.ones(N))
+    assert isinstance(half, DiffMapComp) and isinstance(half.map1, HomothetyMap)
+    assert half.diff_lipschitz_cst == 1.0
+    C = Convolve2D(N, np.ones((3, 3)) / 9, (4, 4))
+    C.lipschitz_cst = C.diff_lipschitz_cst = 0.5
+    F = half * C
+    assert F.diff_lipschitz_cst == 0.25 and F.shape == (1, N)
+    assert SquaredL2Loss(dim=N, data=np.ones(N)).diff_lipschitz_cst == 2
+    assert (3 * L1Norm(N)).scale == 3
+    # L21Norm.__new__ dispatch (penalty.py:525-530)
+    assert isinstance(L21Norm(10, groups=None), L1Norm)
+    assert isinstance(L21Norm(10, groups=np.arange(10)), L1Norm)
+    assert isinstance(L21Norm(10, groups=np.zeros(10)), L2Norm)
+    l21 = L21Norm(10, groups=np.tile(np.arange(5), 2))
+    assert isinstance(l21, L21Norm) and l21.pixel_d == 2
+    assert L21Norm(10, groups=np.repeat(np.arange(5), 2)).pixel_d == 0
+    assert SquaredL2Norm(3).diff_lipschitz_cst == 2
+
+
+@pytest.mark.parametrize('name', pds_case_names())
+def test_pds_construction_matches_reference(name):
+    """Step sizes, momentum and beta from our PDS constructor equal the reference's."""
+    from tests.test_gpu_pds import build
+    c = pds_case(name)
+    pds = build(c, np.float64)
+    assert pds.tau == float(c['tau']) and pds.sigma == float(c['sigma'])
+    assert pds.rho == float(c['rho']) and pds.beta == float(c['beta'])
+    from pycsou_amd.opt.engine import match_pds2d
+    spec = match_pds2d(pds.F, pds.G, pds.H, pds.K, True)
+    fused_expected = ('3d' not in name and 'lap' not in name and '_cen_' not in name and '_bwd_' not in name)
+    assert (spec is not None) == fused_expected
+
+
+def test_pds_validation_errors():
+    from pycsou_amd.func.penalty import L1Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS, APGD
+    from pycsou_amd.func.loss import SquaredL2Loss
+    K = Gradient((4, 4), kind='forward')
+    with pytest.raises(ValueError):
+        PDS(dim=16, H=L1Norm(32), K=K)  # K.lipschitz_cst is inf (proxalgs.py:289-290)
+    with pytest.raises(ValueError):
+        PDS(dim=16, H=L1Norm(31), K=K)
+    with pytest.raises(TypeError):
+        PDS(dim=16, F=3.0)
+    with pytest.raises(ValueError):
+        PDS(dim=15, F=SquaredL2Loss(16, np.zeros(16)))
+    with pytest.raises(TypeError):
+        APGD(dim=16, G='x')
+    K.lipschitz_cst = 2.0
+    p = PDS(dim=16, H=L1Norm(32), K=K, verbose=None)
+    assert p.tau == p.sigma == 0.5 and p.rho == 1
+    p = PDS(dim=16, F=SquaredL2Loss(16, np.zeros(16)), verbose=None)
+    assert p.tau == 1.0 and p.sigma == 0 and p.rho == 0.9 and p.K.lipschitz_cst == 0
+
+
+def test_graft_entry_importable():
+    import importlib
+    m = importlib.import_module('__graft_entry__')
+    assert callable(m.build) and callable(m.smoke)
