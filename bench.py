@@ -1,0 +1,180 @@
+"""PDS TV-deconvolution benchmark (BASELINE.json metric: PDS iters/sec on 4096^2
+TV-deconv; achieved HBM GB/s vs roofline).
+
+Workload: 4096 x 4096 piecewise-constant phantom, 15x15 Gaussian PSF
+(sigma = 2 px, sum 1), y = h*x + 0.01 N(0,1); PDS with F = 1/2 ||Conv x - y||^2,
+K = Gradient(kind='forward'), H = 0.05 * L21Norm (isotropic TV), fp32, built through the
+public pycsou-style API and run by the fused hipGraph engine.  One "step" = one PDS
+iteration (pcs_pds2d_step + pcs_pds_reduce_finalize).
+
+N > 1 (one process per GPU, torch.distributed over RCCL): the image is (4096 N) x 4096,
+row-slab sharded, one 4096^2 slab per rank (weak scaling); every iteration exchanges
+halo rows with the two neighbour ranks and all-reduces the four convergence norms.
+`value` is the whole-job throughput in 4096^2-image PDS iterations per second
+(= N x slab iterations/s).
+
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+METRIC = 'PDS iters/sec on 4096² TV-deconv; achieved HBM GB/s vs roofline at 1/2/4/8 GPU'
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def phantom(shape, n_rect, seed):
+    rng = np.random.default_rng(seed)
+    x = np.zeros(shape, dtype=np.float64)
+    for _ in range(n_rect):
+        lo = [rng.integers(0, s) for s in shape]
+        hi = [min(s, l + rng.integers(max(1, s // 16), max(2, s // 3))) for s, l in zip(shape, lo)]
+        x[tuple(slice(a, b) for a, b in zip(lo, hi))] = rng.uniform(0, 1)
+    return x
+
+
+def gaussian_psf(size=15, sigma=2.0):
+    r = np.arange(size) - (size - 1) / 2
+    g = np.exp(-0.5 * (r / sigma) ** 2)
+    h = np.outer(g, g)
+    return h / h.sum()
+
+
+def build_problem(n0, n1, dtype, seed=0):
+    """The C3 problem through the public API (pycsou scripts look exactly like this)."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    N = n0 * n1
+    xs = torch.as_tensor(phantom((n0, n1), 64, seed).ravel()).to('cuda', dtype)
+    C = Convolve2D(size=N, filter=gaussian_psf(15, 2.0), shape=(n0, n1))
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0  # nonnegative PSF of unit sum: ||Conv|| <= 1
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = C(xs) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
+    K = Gradient(shape=(n0, n1), kind='forward')
+    # exact ||grad_fwd|| on an n0 x n1 grid (eigenvalues of the Neumann Laplacian)
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(4 * np.sin(np.pi * (n0 - 1) / (2 * n0)) ** 2
+                                                            + 4 * np.sin(np.pi * (n1 - 1) / (2 * n1)) ** 2))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
+    H = 0.05 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2))
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+               z0=torch.zeros(2 * N, dtype=dtype, device='cuda'), verbose=None)
+
+
+def cpu_baseline(n, iters):
+    """The reference CPU op sequence (oracle restatement: NumPy temporaries, SciPy FFT
+    convolution, np.linalg.norm diagnostics into a pandas DataFrame, deepcopy of the
+    iterand) on the same C3 problem at full size, fp64 (the reference default)."""
+    from oracle import pycsou_ref as OR
+    from oracle import pylops1 as P
+    N = n * n
+    xs = phantom((n, n), 64, 0).ravel()
+    h = gaussian_psf(15, 2.0)
+    Cr = P.Convolve2D(N, h, (n, n), offset=(7, 7), method='fft')
+    y = Cr.matvec(xs) + 0.01 * np.random.default_rng(1).standard_normal(N)
+    Kr = P.Gradient((n, n), edge=True, kind='forward')
+    Klip = float(np.sqrt(8 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    tau, sigma = OR.pds_step_sizes(1.0, Klip)
+    hprox = OR.postcomp(lambda v, t: OR.prox_l21_pixel(v, t, 2), 0.05)
+    t0 = time.perf_counter()
+    OR.pds(lambda x: Cr.rmatvec((2 * (Cr.matvec(x) + (-y))) * 0.5), lambda v, t: v, Kr.matvec, Kr.rmatvec,
+           lambda w, s: OR.fenchel_prox(hprox, w, s), tau, sigma, 0.9, np.zeros(N), np.zeros(2 * N),
+           max_iter=iters - 1, min_iter=iters - 1, accuracy_threshold=0.0, pandas_diagnostics=True)
+    dt = time.perf_counter() - t0
+    return {'value': iters / dt, 'unit': 'it/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{iters} PDS iterations of the same 4096x4096 TV-deconvolution (fp64, reference op '
+                      f'sequence incl. SciPy FFT convolution, vectorised pixel-L21, pandas diagnostics, deepcopy) '
+                      f'in {dt:.1f} s on 1 host core'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--size', type=int, default=4096)
+    ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
+    ap.add_argument('--cpu-iters', type=int, default=3)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dtype = torch.float32 if args.dtype == 'f32' else torch.float64
+    n = args.size
+    K = max(2, args.steps + (args.steps % 2))
+    W = max(0, args.warmup + (args.warmup % 2))
+    # iterations per captured graph: the largest even divisor of both K and W (<= 50)
+    chunk = max(c for c in range(2, min(K, 50) + 1, 2) if K % c == 0 and W % c == 0)
+
+    if world > 1:
+        from pycsou_amd.parallel import slab_bench
+        res = slab_bench(n, n, dtype, K, W, chunk, world, rank)
+    else:
+        pds = build_problem(n, n, dtype)
+        from pycsou_amd.opt.engine import PDS2DEngine
+        spec = pds._fused_spec()
+        assert spec is not None and spec['fkind'] == 2, 'C3 problem must take the fused separable engine'
+        eng = PDS2DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+        eng.prepare_fixed(W + K + 4, chunk)
+        for _ in range(W // chunk):
+            eng.replay()
+        torch.cuda.synchronize()
+        t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t_start.record()
+        for _ in range(K // chunk):
+            eng.replay()
+        t_end.record()
+        torch.cuda.synchronize()
+        ms = t_start.elapsed_time(t_end) / K
+        kern_ms = eng.time_step_kernel(min(K, 100))
+        it_done = int(eng.ctrl.view(torch.int32)[0].item())
+        assert it_done == W + K, (it_done, W, K)
+        res = {'ms_per_step': ms, 'kernel_ms': kern_ms, 'nblocks': eng.nblocks}
+
+    if rank == 0:
+        elem = 4 if dtype == torch.float32 else 8
+        N = n * n
+        alg_bytes = 7 * N * elem  # (2d+3) N words: read x, z (2N), y; write x', z' (2N)
+        ms = res['ms_per_step']
+        value = world / (ms * 1e-3)  # 4096^2-image iterations per second, whole job
+        achieved = alg_bytes / (res['kernel_ms'] * 1e-3) / 1e9
+        out = {
+            'metric': METRIC, 'value': round(value, 3), 'unit': 'it/s', 'n_gpus': world, 'steps': K, 'warmup': W,
+            'ms_per_step': round(ms, 5), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': args.dtype, 'data': 'synthetic',
+            'config': {'workload': f'C3 TV-deconvolution {n}x{n} per GPU ({n * world}x{n} global, row slabs), '
+                                   f'15x15 Gaussian PSF sigma=2 (rank-1: separable passes), isotropic TV '
+                                   f'0.05*L21Norm, Gradient(kind=forward), PDS fused step, hipGraph chunks of '
+                                   f'{chunk} iterations',
+                       'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single'},
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'kernel': 'pcs_pds2d_step (k_pds2d<float,2,7,32>)',
+                         'kernel_ms': round(res['kernel_ms'], 5), 'alg_bytes_per_launch': alg_bytes},
+            'iteration_GBps': round(alg_bytes / (ms * 1e-3) / 1e9, 1),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
+        else:
+            out['cpu_baseline'] = None
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -167,7 +167,8 @@ __global__ __launch_bounds__(256) void k_reduce_stage2(const double* __restrict_
 
 template <typename T>
 static int reduce(int kind, const void* x, const void* y, int64_t n, double* out, void* ws, hipStream_t st) {
-  if (!x || !out || !ws || n < 0 || kind < 0 || kind > 3 || (kind >= 2 && !y)) return PCS_EINVAL;
+  if (!out || !ws || n < 0 || kind < 0 || kind > 3) return PCS_EINVAL;
+  if (n > 0 && (!x || (kind >= 2 && !y))) return PCS_EINVAL;
   const unsigned g = grid_for(n, 256, kRedBlocks);
   k_reduce_stage1<T><<<g, 256, 0, st>>>(kind, (const T*)x, (const T*)y, n, (double*)ws);
   k_reduce_stage2<<<1, 256, 0, st>>>((const double*)ws, (int)g, out);

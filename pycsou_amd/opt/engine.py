@@ -128,6 +128,7 @@ class PDS2DEngine:
             else:
                 fk = L.PCS_F_GRADBUF
                 self.conv = conv
+                conv._h.get(dtype), conv._hf.get(dtype)  # device PSF copies exist before capture
                 self.R = torch.empty(self.N, dtype=dtype, device=dev)
                 self.Gb = torch.empty(self.N, dtype=dtype, device=dev)
                 a.gbuf = self.Gb.data_ptr()
@@ -162,6 +163,42 @@ class PDS2DEngine:
     def _chunk(self, hist):
         for i in range(self.chunk):
             self._iteration(i % 2, hist)
+
+    # ---- fixed-count loop for benchmarking (bench.py): no early stop, optional per-step events
+    def prepare_fixed(self, total_iters, chunk):
+        """Device state for `total_iters` iterations that never stop early, captured in
+        graphs of `chunk` (even) iterations."""
+        self.chunk = chunk
+        hist_len = 2 * (total_iters + 1) + 2
+        self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(total_iters), int(total_iters), -1.0, 1, hist_len,
+                                        L.stream()), 'pcs_ctrl_init2')
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._chunk(self.hist)
+        torch.cuda.synchronize()
+
+    def replay(self):
+        self.graph.replay()
+
+    def time_step_kernel(self, n, stream=None):
+        """Average duration (ms) of the fused step kernel over `n` eager launches, measured
+        with HIP events on the stream the kernel runs on."""
+        a = self.args
+        st = torch.cuda.current_stream() if stream is None else stream
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        ctrl, a.ctrl = a.ctrl, None  # always run (no stop-flag check) while timing
+        for i in range(n):
+            p = i % 2
+            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            evs[i][0].record(st)
+            L.check(self.lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step')
+            evs[i][1].record(st)
+        torch.cuda.synchronize()
+        a.ctrl = ctrl
+        return float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
     def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
         total = max(min_iter, max_iter) + 1

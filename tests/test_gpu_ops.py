@@ -35,7 +35,7 @@ def A():
 
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
-@pytest.mark.parametrize('shape', [(64, 64), (63, 65), (1, 17), (5, 6, 7), (16, 17, 18), (129,)])
+@pytest.mark.parametrize('shape', [(64, 64), (63, 65), (2, 17), (5, 6, 7), (16, 17, 18), (129,)])
 @pytest.mark.parametrize('kind', ['forward', 'backward', 'centered'])
 @pytest.mark.parametrize('edge', [True, False])
 def test_gradient(A, dtype, shape, kind, edge):

@@ -175,7 +175,8 @@ def test_pds_fused_4096_properties(dtype):
         est, _, diag = pds.iterate()
         assert pds.iter == 3
         out.append((est['primal_variable'], est['dual_variable'], diag))
-    tol = 1e-12 if dtype == np.float64 else 2e-6
+    # fused = separable 15+15-tap passes, generic = direct 225-tap conv: fp32 summation-order rounding
+    tol = 1e-12 if dtype == np.float64 else 3e-5
     assert float(torch.linalg.vector_norm(out[0][0] - out[1][0]) / torch.linalg.vector_norm(out[1][0])) < tol
     assert float(torch.linalg.vector_norm(out[0][1] - out[1][1]) / torch.linalg.vector_norm(out[1][1])) < tol
     assert torch.isfinite(out[0][0]).all()
