@@ -5,7 +5,7 @@ SRC := $(wildcard pycsou_amd/csrc/*.hip)
 HDR := $(wildcard pycsou_amd/csrc/*.hpp) include/pycsou_hip.h
 LIB := pycsou_amd/lib/libpycsou_hip.so
 OBJ := $(patsubst pycsou_amd/csrc/%.hip,build/%.o,$(SRC))
-FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
+FLAGS := --offload-arch=$(ARCH) -O3 -fno-slp-vectorize -fPIC -std=c++17 -Wall -Wno-unused-function -Iinclude
 
 all: $(LIB)
 

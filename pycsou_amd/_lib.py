@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  -- must be imported first: its libamdhip64.so.7 is the one we bind to
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'lib', 'libpycsou_hip.so')
+# PCS_LIB_PATH: diagnostics only (e.g. an ablation build of the same sources).
+LIB_PATH = os.environ.get('PCS_LIB_PATH') or os.path.join(_HERE, 'lib', 'libpycsou_hip.so')
 
 PCS_F32, PCS_F64 = 0, 1
 PCS_FORWARD, PCS_BACKWARD, PCS_CENTERED = 0, 1, 2

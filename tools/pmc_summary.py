@@ -1,0 +1,14 @@
+"""Average PMC counters per kernel from rocprofv3 counter_collection CSVs."""
+import csv, sys, collections, glob
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for path in sys.argv[1:]:
+    for f in glob.glob(path):
+        for r in csv.DictReader(open(f)):
+            k = r['Kernel_Name'][:60]
+            vals[k][r['Counter_Name']].append(float(r['Counter_Value']))
+for k, d in vals.items():
+    if 'k_pds2d' not in k and 'reduce' not in k and 'conv' not in k and 'grad' not in k:
+        continue
+    print(k)
+    for c, v in sorted(d.items()):
+        print(f'   {c:28s} {sum(v)/len(v):16.1f}  (n={len(v)})')
