@@ -146,11 +146,15 @@ typedef struct {
   double tau, sigma, rho, lam, step0, step1, seg_a, seg_b;
   const void* x; void* xn; const void* z; void* zn; const void* y; const void* gbuf;
   double* partials;       /* [nblocks][4] */
-  const int32_t* ctrl;    /* device control block (pcs_ctrl_*) ; NULL = always run */
+  void* ctrl;             /* device control block (pcs_ctrl_*) ; NULL = always run */
+  double* hist;           /* non-NULL: reduce the partials and run pcs_pds_finalize inside the
+                             step launch (single GPU); NULL: only write `partials` */
+  void* ws;               /* with hist: pcs_pds2d_ws_bytes() bytes, zeroed once before first use */
 } pcs_pds2d_args;
 
 int pcs_pds2d_halo_x(int half);
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
+int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a);
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
 
 /* Device control block for the hipGraph-captured loop:

@@ -35,7 +35,7 @@ class PdsArgs(ctypes.Structure):
                 ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
                 ('step0', _c_dbl), ('step1', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
-                ('partials', _vp), ('ctrl', _vp)]
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
 
 
 # name -> (restype, argtypes)
@@ -65,6 +65,7 @@ _SIGS = {
     'pcs_reduce': (_c_int, [_c_int, _c_int, _vp, _vp, _c_i64, _vp, _vp, _vp]),
     'pcs_pds2d_halo_x': (_c_int, [_c_int]),
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
+    'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
     'pcs_ctrl_bytes': (_c_i64, []),
     'pcs_ctrl_init': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _vp]),

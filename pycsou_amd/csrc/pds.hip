@@ -13,13 +13,6 @@
 namespace pcs {
 
 // ---------------------------------------------------------------- loop control
-struct Ctrl {
-  int32_t it, stopped, min_iter, max_iter, has_dual, hist_len, pad0, pad1;
-  double thr;
-  double pad2;
-};
-static_assert(sizeof(Ctrl) == 48, "ctrl layout");
-
 __global__ void k_ctrl_init(Ctrl* c, int min_iter, int max_iter, double thr, int has_dual, int hist_len) {
   c->it = 0;
   c->min_iter = min_iter;
@@ -30,23 +23,6 @@ __global__ void k_ctrl_init(Ctrl* c, int min_iter, int max_iter, double thr, int
   c->pad0 = c->pad1 = 0;
   const double inf = __builtin_huge_val();
   c->stopped = !((0 <= min_iter) || (0 <= max_iter && inf > thr));
-}
-
-__device__ __forceinline__ void finalize_from(const double* v, Ctrl* c, double* hist) {
-  const int it = c->it;
-  const double inf = __builtin_huge_val();
-  // update_diagnostics: ||old - new|| / ||old||, inf if ||old|| == 0 (proxalgs.py:372-383)
-  const double rp = (v[1] == 0.0) ? inf : sqrt(v[0]) / sqrt(v[1]);
-  const double rd = (v[3] == 0.0) ? inf : sqrt(v[2]) / sqrt(v[3]);
-  if (2 * it + 1 < c->hist_len) {
-    hist[2 * it] = rp;
-    hist[2 * it + 1] = rd;
-  }
-  const int nx = it + 1;
-  c->it = nx;
-  // while ((iter <= max_iter) and (stopping_metric() > thr)) or (iter <= min_iter)
-  const bool run = (nx <= c->min_iter) || (nx <= c->max_iter && rp > c->thr);
-  if (!run || 2 * nx + 1 >= c->hist_len) c->stopped = 1;
 }
 
 // Sum [np][4] partials in a fixed order (deterministic): 1024 threads, 4 independent
@@ -150,7 +126,8 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   P.seg_b = (T)a->seg_b;
   k_pds2d<T, FK, H, TH, NT><<<(unsigned)ntiles, NT, 0, st>>>(
       (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->y, (const T*)a->gbuf, (const T*)a->taps0,
-      (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, a->ctrl, tiles_x, (int)ntiles);
+      (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, tiles_x,
+      (int)ntiles);
   return launch_status();
 }
 
@@ -192,8 +169,14 @@ int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);
 }
 
+int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a) {
+  const int64_t nb = pcs_pds2d_nblocks(a);
+  return nb < 0 ? -1 : red_ws_bytes(nb);
+}
+
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
   if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
+  if (a->hist && (!a->ws || !a->ctrl || !aligned16(a->ws) || !aligned16(a->partials))) return PCS_EINVAL;
   if (a->n0 < 1 || a->n1 < 1 || a->rows < 1 || a->row0 < 0 || a->row0 + a->rows > a->n0) return PCS_EINVAL;
   if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return PCS_EINVAL;
   if (a->gkind < PCS_G_NULL || a->gkind > PCS_G_SEGMENT) return PCS_EINVAL;

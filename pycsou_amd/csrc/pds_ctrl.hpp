@@ -1,0 +1,117 @@
+// Device-side loop control of the captured PDS loop (replaces the host `while` of
+// GenericIterativeAlgorithm.iterate, pycsou/core/solver.py:65-76, and the diagnostics of
+// PrimalDualSplitting.update_diagnostics, pycsou/opt/proxalgs.py:366-394), and the
+// in-kernel deterministic reduction of the per-workgroup norm partials.
+#pragma once
+
+#include "common.hpp"
+
+namespace pcs {
+
+struct Ctrl {
+  int32_t it, stopped, min_iter, max_iter, has_dual, hist_len, pad0, pad1;
+  double thr;
+  double pad2;
+};
+static_assert(sizeof(Ctrl) == 48, "ctrl layout");
+
+// From the four global sums (||x_old - x||^2, ||x_old||^2, ||z_old - z||^2, ||z_old||^2)
+// record the relative improvements of iteration `it`, advance it, and set the sticky stop
+// flag exactly when the reference loop would exit.
+__device__ __forceinline__ void finalize_from(const double* v, Ctrl* c, double* hist) {
+  const int it = c->it;
+  const double inf = __builtin_huge_val();
+  // ||old - new|| / ||old||, inf if ||old|| == 0 (proxalgs.py:372-383)
+  const double rp = (v[1] == 0.0) ? inf : sqrt(v[0]) / sqrt(v[1]);
+  const double rd = (v[3] == 0.0) ? inf : sqrt(v[2]) / sqrt(v[3]);
+  if (2 * it + 1 < c->hist_len) {
+    hist[2 * it] = rp;
+    hist[2 * it + 1] = rd;
+  }
+  const int nx = it + 1;
+  c->it = nx;
+  // while ((iter <= max_iter) and (stopping_metric() > thr)) or (iter <= min_iter)
+  const bool run = (nx <= c->min_iter) || (nx <= c->max_iter && rp > c->thr);
+  if (!run || 2 * nx + 1 >= c->hist_len) c->stopped = 1;
+}
+
+// ---- in-kernel reduction (hand-off form R1 of cdna_hip_programming.md G16: write-through
+// `sc1` payload stores drained by s_waitcnt vmcnt(0) before an agent-scope counter add,
+// `sc1` payload loads on the consumer side -- no L2 write-back / invalidate fences, which
+// would flush every freshly written x'/z' line of the XCD).
+// Workgroups are grouped by blockIdx in groups of kGrp.  Every workgroup publishes its
+// 4 partials; the last arriver of a group sums the group's partials in lane order and
+// publishes the group sum; the last group sums the group sums in a fixed order and runs
+// finalize_from.  Fixed summation order => bitwise-reproducible diagnostics.
+// Workspace layout: [ngroups][4] doubles (group sums) | (ngroups + 1) uint32 counters,
+// zeroed once before first use; every counter is reset by its last arriver.
+constexpr int kGrp = 64;
+
+__host__ __device__ inline int64_t red_groups(int64_t nblocks) { return (nblocks + kGrp - 1) / kGrp; }
+__host__ __device__ inline int64_t red_ws_bytes(int64_t nblocks) {
+  return red_groups(nblocks) * 4 * (int64_t)sizeof(double) + ((red_groups(nblocks) + 1) * 4 + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// drain this wave's sc1 stores, then count the arrival
+__device__ __forceinline__ unsigned drained_add(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by every thread of every workgroup after thread 0's `part` holds the block sums.
+// `flag` is a 2-int LDS scratch.
+__device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], double* __restrict__ partials,
+                                                    int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag) {
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t ngr = red_groups(nblocks);
+  double* gsum = reinterpret_cast<double*>(ws);
+  unsigned* cnt = reinterpret_cast<unsigned*>(gsum + ngr * 4);
+  const int64_t grp = b / kGrp;
+  const unsigned members = (unsigned)min<int64_t>(kGrp, nblocks - grp * kGrp);
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st_sc1(partials + b * 4 + k, part[k]);
+    flag[0] = (drained_add(&cnt[grp]) == members - 1);
+  }
+  __syncthreads();
+  if (!flag[0]) return;  // uniform
+  // ---- last workgroup of its group: lane j sums member j (wave-order reduction)
+  if (tid < 64) {
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if ((unsigned)tid < members) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ld_sc1(partials + (grp * kGrp + tid) * 4 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = wave_sum(v[k]);
+    if (tid == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) st_sc1(gsum + grp * 4 + k, v[k]);
+      __hip_atomic_store(&cnt[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for next launch
+      flag[1] = (drained_add(&cnt[ngr]) == (unsigned)ngr - 1);
+    }
+  }
+  __syncthreads();
+  if (!flag[1]) return;  // uniform
+  // ---- last group: sum the group sums in a fixed order, then finalize
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t g = tid; g < ngr; g += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] += ld_sc1(gsum + g * 4 + k);
+  }
+  __shared__ double red2[4 * 16];
+  block_sum<4>(v, red2);
+  if (tid == 0) {
+    __hip_atomic_store(&cnt[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    finalize_from(v, ctrl, hist);
+  }
+}
+
+}  // namespace pcs

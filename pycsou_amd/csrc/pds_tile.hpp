@@ -25,6 +25,7 @@
 #pragma once
 
 #include "common.hpp"
+#include "pds_ctrl.hpp"
 
 // Diagnostics only: bit k skips phase k (0 P1, 1 P2, 2 P3, 3 P4, 4 P5, 5 P6, 6 X->LDS,
 // 7 z->LDS) so rocprof counters can be attributed to phases.  Results are wrong.
@@ -470,8 +471,8 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
                                                T* __restrict__ zn, const T* __restrict__ y,
                                                const T* __restrict__ gbuf, const T* __restrict__ taps0,
                                                const T* __restrict__ taps1, int half, Slab s, Params<T> P, int hk,
-                                               int gk, double* __restrict__ partials,
-                                               const int32_t* __restrict__ ctrl, int tiles_x, int ntiles) {
+                                               int gk, double* __restrict__ partials, Ctrl* ctrl,
+                                               double* hist, void* ws, int tiles_x, int ntiles) {
   constexpr bool CONV = (FK == PCS_F_SEPCONV);
   constexpr int TW = 64;
   constexpr int H4 = RU4<H>::value;
@@ -483,8 +484,9 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   __shared__ __attribute__((aligned(16))) T bufX[SZX];
   __shared__ __attribute__((aligned(16))) T bufA[SZA];
   __shared__ double red[4 * (NT / 64)];
+  __shared__ int flag[2];
 
-  if (ctrl != nullptr && ctrl[1] != 0) return;  // loop already stopped (solver.py:65-66)
+  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
 
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent tiles.
   int tile;
@@ -517,7 +519,10 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   else
     pds2d_tile<T, FK, H, TH, NT, false>(x, xn, z, zn, y, gbuf, w0, w1, s, P, hk, gk, t0, c0, bufX, bufA, part);
   block_sum<4>(part, red);
-  if (threadIdx.x == 0) {
+  if (hist != nullptr) {
+    // single launch per iteration: last workgroups reduce + finalize in-kernel
+    reduce_and_finalize(part, partials, ntiles, ws, ctrl, hist, flag);
+  } else if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
   }

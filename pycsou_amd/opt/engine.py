@@ -140,6 +140,11 @@ class PDS2DEngine:
         a.partials = self.partials.data_ptr()
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
+        # in-kernel reduce + finalize (one launch per iteration); counters must start at 0
+        self.fused_finalize = True
+        self.ws = torch.zeros(int(self.lib.pcs_pds2d_ws_bytes(ctypes.byref(a))) // 8 + 2, dtype=torch.float64,
+                              device=dev)
+        a.ws = self.ws.data_ptr()
         self.graph = None
         self.hist = None
         self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
@@ -156,9 +161,11 @@ class PDS2DEngine:
                                    c.kw, c.kh - 1 - c.off[0], c.kw - 1 - c.off[1], None, 0.0, st), 'pcs_conv2d')
         a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
         a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        a.hist = hist.data_ptr() if self.fused_finalize else None
         L.check(lib.pcs_pds2d_step(ctypes.byref(a), st), 'pcs_pds2d_step')
-        L.check(lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl), L.ptr(hist), st),
-                'pcs_pds_reduce_finalize')
+        if not self.fused_finalize:
+            L.check(lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl), L.ptr(hist),
+                                                st), 'pcs_pds_reduce_finalize')
 
     def _chunk(self, hist):
         for i in range(self.chunk):
@@ -187,8 +194,14 @@ class PDS2DEngine:
         with HIP events on the stream the kernel runs on."""
         a = self.args
         st = torch.cuda.current_stream() if stream is None else stream
+        # fresh loop state that runs all n launches (the in-kernel reduce + finalize is timed too)
+        n = min(n, (self.hist.numel() - 2) // 2 - 1)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
-        ctrl, a.ctrl = a.ctrl, None  # always run (no stop-flag check) while timing
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, int(self.hist.numel()), L.stream()),
+                'pcs_ctrl_init2')
+        ctrl, hist = a.ctrl, a.hist
+        if not self.fused_finalize:
+            a.hist = None
         for i in range(n):
             p = i % 2
             a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
@@ -197,7 +210,7 @@ class PDS2DEngine:
             L.check(self.lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step')
             evs[i][1].record(st)
         torch.cuda.synchronize()
-        a.ctrl = ctrl
+        a.ctrl, a.hist = ctrl, hist
         return float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
     def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
