@@ -95,6 +95,39 @@ def cpu_baseline(n, iters):
                       f'in {dt:.1f} s on 1 host core'}
 
 
+def slab_bench(n, dtype, K, W, world):
+    """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
+    (barrier + synchronize on both sides; the caller takes the max over ranks)."""
+    from pycsou_amd.parallel import DistComm, SlabPDS2D
+    pds = build_problem(n * world, n, dtype)
+    comm = DistComm() if world > 1 else None
+    eng = SlabPDS2D.from_pds(pds, comm, rank=0 if comm is None else None, world=1 if comm is None else None)
+    del pds
+    torch.cuda.empty_cache()
+    total = W + K + 4
+    eng.init_loop(total, total, -1.0)  # fixed count: the loop never stops early
+    eng.advance(W)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.advance(K)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    it_done = eng.iterations()
+    assert it_done == W + K, (it_done, W, K)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kern_ms = eng.time_step_kernel(min(K, 100))
+    return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'nblocks': eng.nblocks}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -104,6 +137,8 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
+                    help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -119,9 +154,8 @@ def main():
     # iterations per captured graph: the largest even divisor of both K and W (<= 50)
     chunk = max(c for c in range(2, min(K, 50) + 1, 2) if K % c == 0 and W % c == 0)
 
-    if world > 1:
-        from pycsou_amd.parallel import slab_bench
-        res = slab_bench(n, n, dtype, K, W, chunk, world, rank)
+    if world > 1 or args.engine == 'slab':
+        res = slab_bench(n, dtype, K, W, world)
     else:
         pds = build_problem(n, n, dtype)
         from pycsou_amd.opt.engine import PDS2DEngine
@@ -157,8 +191,10 @@ def main():
             'dtype': args.dtype, 'data': 'synthetic',
             'config': {'workload': f'C3 TV-deconvolution {n}x{n} per GPU ({n * world}x{n} global, row slabs), '
                                    f'15x15 Gaussian PSF sigma=2 (rank-1: separable passes), isotropic TV '
-                                   f'0.05*L21Norm, Gradient(kind=forward), PDS fused step, hipGraph chunks of '
-                                   f'{chunk} iterations',
+                                   f'0.05*L21Norm, Gradient(kind=forward), PDS fused step, '
+                                   + (f'hipGraph chunks of {chunk} iterations' if 'nblocks' in res and world == 1
+                                      and args.engine != 'slab' else
+                                      'slab engine: per-iteration RCCL all-gather of 4 sums + halo exchange'),
                        'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,

@@ -1,0 +1,352 @@
+"""Row-slab sharding of the fused 2-D PDS loop over GPUs.
+
+The reference solves one image on one host (``PrimalDualSplitting`` in
+``pycsou/opt/proxalgs.py:343-394``); here an ``n0 x n1`` image (C order) is split into
+contiguous row slabs, one per rank (one process per GPU).  Rank ``r`` stores rows
+``[row0 - h, row0 + rows + h)`` of every array the step reads at a row offset and computes
+only its own rows.  One iteration is
+
+    pcs_pds2d_step (slab mode)      x, z  ->  x', z' on own rows + per-block norm partials
+    pcs_reduce_partials             -> 4 local sums, fixed order
+    all-gather of the 4 sums        (RCCL, 32 B per rank)
+    pcs_pds_reduce_finalize         -> the same global sums, history entry and stop flag
+                                       on every rank (sums added in rank order)
+    halo exchange                   x' (hx rows), z0'/z1' (hz rows) with the two
+                                    neighbour ranks (RCCL point-to-point, one group call)
+
+Halo depths follow the step's stencil reach: x' at row i reads x rows i-2H-1 .. i+2H+1
+(conv^T conv of half-width H plus the forward difference of u = 2x' - x), y rows
+i-H-1 .. i+H+1 and z rows i-1 .. i+1, hence hx = 2H+1, hy = H+1, hz = 1 (H = 0 without
+a convolution).  y is static: its halo is sliced once from the global data.
+
+Per-pixel arithmetic is the same as on one GPU, so x and z are bitwise identical to the
+single-GPU engine; only the order in which the four diagnostic sums are added differs
+(per-rank partial sums), which moves the relative improvements by a few ulps.
+
+Transport: ``DistComm`` wraps a ``torch.distributed`` process group -- NCCL (= RCCL on
+ROCm) with device buffers in production; any other backend (gloo) is host-staged, which
+is what the multi-process tests on a single GPU use.  ``run_local`` drives several slabs
+of one process (one GPU) with device-to-device halo copies for the parity tests.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import _lib as L
+from .. import _ops as O
+
+
+def row_split(n0, world, rank):
+    """Balanced contiguous split of ``n0`` rows: (row0, rows) of ``rank``."""
+    base, rem = divmod(int(n0), int(world))
+    rows = base + (1 if rank < rem else 0)
+    row0 = rank * base + min(rank, rem)
+    return row0, rows
+
+
+class DistComm:
+    """Sum gathering and neighbour halo exchange over a torch.distributed group."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.staged = dist.get_backend(group) != 'nccl'
+
+    def _peer(self, r):
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def allgather(self, src, dst):
+        """dst[4 r : 4 r + 4] = src of rank r."""
+        if self.world == 1:
+            dst.copy_(src)
+        elif self.staged:
+            parts = [torch.empty_like(src, device='cpu') for _ in range(self.world)]
+            dist.all_gather(parts, src.cpu(), group=self.group)
+            dst.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(dst, src, group=self.group)
+
+    def exchange(self, pairs):
+        """pairs: {peer: [(send_view, recv_view), ...]}; the k-th send to a peer lands in the
+        peer's k-th receive from us."""
+        if not pairs:
+            return
+        if self.staged:
+            if torch.cuda.is_available():
+                torch.cuda.current_stream().synchronize()
+            reqs, back = [], []
+            for peer, lst in sorted(pairs.items()):
+                for k, (s, r) in enumerate(lst):
+                    sh = s.cpu()
+                    rh = torch.empty_like(r, device='cpu')
+                    reqs.append(dist.isend(sh, self._peer(peer), group=self.group, tag=k))
+                    reqs.append(dist.irecv(rh, self._peer(peer), group=self.group, tag=k))
+                    back.append((r, rh, sh))
+            for q in reqs:
+                q.wait()
+            for r, rh, _ in back:
+                r.copy_(rh)
+            return
+        ops = []
+        for peer, lst in sorted(pairs.items()):
+            for s, r in lst:
+                ops.append(dist.P2POp(dist.isend, s, self._peer(peer), self.group))
+                ops.append(dist.P2POp(dist.irecv, r, self._peer(peer), self.group))
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+
+
+class SlabLayout:
+    """Row geometry of one rank's slab: arrays hold local rows [-h, rows + h) (C order,
+    n1 columns); a buffer of `ncomp` components stacks them with stride (rows + 2h) n1."""
+
+    def __init__(self, n0, n1, rank, world):
+        self.n0, self.n1, self.rank, self.world = int(n0), int(n1), int(rank), int(world)
+        self.row0, self.rows = row_split(n0, world, rank)
+
+    def window(self, g, h):
+        """Rows [row0 - h, row0 + rows + h) of a global n0*n1 array (zeros outside the image)."""
+        n1 = self.n1
+        out = torch.zeros((self.rows + 2 * h) * n1, dtype=g.dtype, device=g.device)
+        lo, hi = max(0, self.row0 - h), min(self.n0, self.row0 + self.rows + h)
+        d = lo - (self.row0 - h)
+        out[d * n1:(d + hi - lo) * n1] = g[lo * n1:hi * n1]
+        return out
+
+    def rows_view(self, buf, h, r0, r1, comp=0):
+        """Local rows [r0, r1) (own-row coordinates) of component `comp` of a halo'd buffer."""
+        n1 = self.n1
+        base = comp * (self.rows + 2 * h) * n1
+        return buf[base + (r0 + h) * n1: base + (r1 + h) * n1]
+
+    def halo_pairs(self, bufs):
+        """bufs: [(buffer, h, comp), ...] -> {peer: [(send, recv), ...]}: own boundary rows go
+        to the neighbour's halo, the neighbour's boundary rows fill ours."""
+        pairs = {}
+        R = self.rows
+        if self.rank > 0:
+            pairs[self.rank - 1] = [(self.rows_view(b, h, 0, h, c), self.rows_view(b, h, -h, 0, c))
+                                    for b, h, c in bufs]
+        if self.rank < self.world - 1:
+            pairs[self.rank + 1] = [(self.rows_view(b, h, R - h, R, c), self.rows_view(b, h, R, R + h, c))
+                                    for b, h, c in bufs]
+        return pairs
+
+
+class SlabPDS2D:
+    """One rank's slab of a fused 2-D PDS problem.
+
+    ``spec`` is the global problem's engine spec (``PDS._fused_spec()``: shape, H/G kinds,
+    data shift, convolution); ``x0`` / ``z0`` are the global starting points (z0 stacked
+    as [D0 z; D1 z], each ``n0*n1``).  Only this rank's rows (+ halos) are kept.
+    """
+
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, rank, world, comm=None, chunk=16):
+        self.lib = L.gpu()
+        self.comm = comm
+        self.rank, self.world = int(rank), int(world)
+        self.dtype = dtype
+        n0, n1 = spec['shape']
+        self.n0, self.n1 = n0, n1
+        self.lay = lay = SlabLayout(n0, n1, rank, world)
+        self.row0, self.rows = lay.row0, lay.rows
+        fk = spec['fkind']
+        a = L.PdsArgs()
+        a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+        a.hkind, a.gkind = spec['hkind'], spec['gkind']
+        a.n0, a.n1, a.row0, a.rows = n0, n1, self.row0, self.rows
+        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+        a.step0, a.step1 = spec['steps']
+        a.seg_a, a.seg_b = spec['seg']
+        dev = torch.device('cuda', torch.cuda.current_device())
+        half = 0
+        if fk == L.PCS_F_SEPCONV:
+            sep = spec['conv'].separable(rtol=2e-7 if dtype == torch.float32 else 1e-13)
+            if sep is None:
+                raise ValueError('row-slab PDS needs a separable (rank-1) PSF; non-separable convolutions run '
+                                 'on one GPU (PDS2DEngine)')
+            t0, t1, half = sep
+            self.taps = [torch.as_tensor(t0).to(device=dev, dtype=dtype),
+                         torch.as_tensor(t1).to(device=dev, dtype=dtype)]
+            a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
+            a.half = half
+        elif fk not in (L.PCS_F_NULL, L.PCS_F_DENOISE):
+            raise ValueError(f'row-slab PDS does not support fkind {fk}')
+        a.fkind = fk
+        self.fkind = fk
+        # halo depths: the tier the kernel uses for `half` sets its reach
+        hx = int(self.lib.pcs_pds2d_halo_x(half)) if fk == L.PCS_F_SEPCONV else 1
+        hy = (hx - 1) // 2 + 1 if fk == L.PCS_F_SEPCONV else 1
+        hz = 1
+        if world > 1 and self.rows < max(hx, hy, hz):
+            raise ValueError(f'slab of {self.rows} rows is thinner than its halo ({hx} rows)')
+        self.hx, self.hy, self.hz = hx, hy, hz
+        a.halo_x, a.halo_y, a.halo_z = hx, hy, hz
+        N = n0 * n1
+        self.X = [lay.window(O.to_dev(x0, dtype), hx) for _ in range(2)]
+        z0d = O.to_dev(z0, dtype)
+        self.Z = [torch.cat([lay.window(z0d[:N], hz), lay.window(z0d[N:], hz)]) for _ in range(2)]
+        if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV):
+            self.y = lay.window(-O.to_dev(spec['shift'], dtype), hy)  # y = -shift, exactly
+            a.y = self.y.data_ptr()
+        self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
+        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+        a.partials = self.partials.data_ptr()
+        a.hist, a.ws = None, None
+        self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
+        a.ctrl = self.ctrl.data_ptr()
+        self.args = [self._args_for(a, p) for p in (0, 1)]
+        self.halos = [lay.halo_pairs([(self.X[q], hx, 0), (self.Z[q], hz, 0), (self.Z[q], hz, 1)]) for q in (0, 1)]
+        self.hist = None
+        self.chunk = max(1, int(chunk))
+
+    @classmethod
+    def from_pds(cls, pds, comm, rank=None, world=None, chunk=16):
+        """This rank's slab of a PDS problem built with the public API on the global image
+        (every rank builds the same problem, as a single-host script would)."""
+        spec = pds._fused_spec()
+        if spec is None:
+            raise ValueError('problem does not match the fused 2-D PDS engine (see opt/engine.match_pds2d)')
+        rank = comm.rank if rank is None else rank
+        world = comm.world if world is None else world
+        return cls(spec, pds._compute_dtype(), pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank, world, comm, chunk)
+
+    def _args_for(self, a, p):
+        b = L.PdsArgs()
+        ctypes.pointer(b)[0] = a
+        b.x, b.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+        b.z, b.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        return b
+
+    # ---- one iteration, split in phases (run_local interleaves them across slabs)
+    def _compute(self, p):
+        st = L.stream()
+        L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args[p]), st), 'pcs_pds2d_step')
+        L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), self.nblocks, L.ptr(self.sums), st),
+                'pcs_reduce_partials')
+
+    def _finalize(self):
+        L.check(self.lib.pcs_pds_reduce_finalize(L.ptr(self.gathered), self.world, L.ptr(self.ctrl), L.ptr(self.hist),
+                                                 L.stream()), 'pcs_pds_reduce_finalize')
+
+    def iteration(self, p):
+        if self.world == 1:  # one slab = the whole image: no transport
+            st = L.stream()
+            L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args[p]), st), 'pcs_pds2d_step')
+            L.check(self.lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl),
+                                                     L.ptr(self.hist), st), 'pcs_pds_reduce_finalize')
+            return
+        self._compute(p)
+        self.comm.allgather(self.sums, self.gathered)
+        self._finalize()
+        self.comm.exchange(self.halos[1 - p])
+
+    # ---- loops
+    def init_loop(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        total = max(min_iter, max_iter) + 1
+        hist_len = 2 * total + 2
+        if self.hist is None or self.hist.numel() < hist_len:
+            self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
+        self.hist.fill_(float('nan'))
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
+                                        int(has_dual), int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
+        self._p = 0
+        return total
+
+    def advance(self, k):
+        """Enqueue k iterations (no host synchronisation)."""
+        for _ in range(k):
+            self.iteration(self._p)
+            self._p ^= 1
+
+    def stopped(self):
+        return int(self.ctrl.view(torch.int32)[1].item()) != 0
+
+    def iterations(self):
+        return int(self.ctrl.view(torch.int32)[0].item())
+
+    def result(self):
+        """(n_iter, own rows of x, own rows of z (2 components), hist [n, 2])."""
+        torch.cuda.synchronize()
+        n = self.iterations()
+        q = n % 2
+        x = self.lay.rows_view(self.X[q], self.hx, 0, self.rows).clone()
+        z = torch.cat([self.lay.rows_view(self.Z[q], self.hz, 0, self.rows, c) for c in (0, 1)])
+        h = self.hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
+        return n, x, z, h
+
+    def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        """The reference loop (solver.py:65-76) across all ranks: every rank holds the
+        same stop flag, so every rank leaves after the same iteration."""
+        total = self.init_loop(max_iter, min_iter, accuracy_threshold, has_dual)
+        done = 0
+        while done < total:
+            k = min(self.chunk, total - done)
+            self.advance(k)
+            done += k
+            if self.stopped():
+                break
+        return self.result()
+
+    def time_step_kernel(self, n):
+        """Average duration (ms) of the slab step kernel over n eager launches (HIP events
+        on the launching stream); leaves x/z advanced by n iterations of ping-pong."""
+        st = torch.cuda.current_stream()
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, 2 * n + 6, L.stream()),
+                'pcs_ctrl_init2')
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for i in range(n):
+            evs[i][0].record(st)
+            L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args[i % 2]), L.stream()), 'pcs_pds2d_step')
+            evs[i][1].record(st)
+        torch.cuda.synchronize()
+        return float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+
+def run_local(slabs, max_iter, min_iter, accuracy_threshold):
+    """Drive all slabs of one image inside one process (device-to-device halo copies);
+    the per-iteration phase order is the distributed one."""
+    total = None
+    for s in slabs:
+        total = s.init_loop(max_iter, min_iter, accuracy_threshold)
+    by_rank = {s.rank: s for s in slabs}
+    for i in range(total):
+        p = i % 2
+        for s in slabs:
+            s._compute(p)
+        g = torch.cat([s.sums for s in slabs])
+        for s in slabs:
+            s.gathered.copy_(g)
+            s._finalize()
+        for s in slabs:
+            for peer, lst in s.halos[1 - p].items():
+                back = by_rank[peer].halos[1 - p][s.rank]
+                for (_, recv), (send, _) in zip(lst, back):
+                    recv.copy_(send)
+        if (i + 1) % 8 == 0 and slabs[0].stopped():
+            break
+    return [s.result() for s in slabs]
+
+
+def gather_rows(local, n0, n1, world, rank, comm):
+    """Assemble the global n0*n1 array from every rank's own rows (all ranks get it)."""
+    if world == 1:
+        return local
+    counts = [row_split(n0, world, r)[1] * n1 for r in range(world)]
+    mx = max(counts)
+    buf = torch.zeros(mx, dtype=local.dtype, device=local.device)
+    buf[:local.numel()] = local
+    if comm.staged:
+        parts = [torch.empty(mx, dtype=local.dtype) for _ in range(world)]
+        dist.all_gather(parts, buf.cpu(), group=comm.group)
+        parts = [t.to(local.device) for t in parts]
+    else:
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=comm.group)
+    return torch.cat([t[:c] for t, c in zip(parts, counts)])

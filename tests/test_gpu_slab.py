@@ -1,0 +1,134 @@
+"""Row-slab (multi-GPU) PDS against the single-GPU fused engine and the reference.
+
+Slabs of one image are driven (a) inside one process on one GPU (`run_local`,
+device-to-device halos) and (b) by two processes sharing the GPU over a gloo process
+group (host-staged halos; the same DistComm code the RCCL path uses, minus the NCCL
+calls).  The per-pixel arithmetic does not depend on the slab split, so x and z must be
+bitwise identical to the single-GPU engine; the diagnostic sums are added per rank, so
+the history agrees to 1e-12 relative and the iteration count exactly.
+"""
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests.cases import pds_case, rel
+from tests.test_gpu_pds import build
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SLAB_CASES = ['denoise2d_l21_fwd_64', 'denoise2d_l1_fwd_63x65', 'deconv2d_l21_fwd_64_psf15', 'deconv2d_l21_fwd_64_seg',
+              'denoise2d_l21_fwd_32_stop']
+
+
+def _single(c, dtype):
+    pds = build(c, dtype, engine='fused')
+    est, _, diag = pds.iterate()
+    h = pds._engine.hist[:2 * pds.iter].cpu().numpy().reshape(-1, 2)
+    return pds.iter, pds._engine.X[pds.iter % 2].clone(), pds._engine.Z[pds.iter % 2].clone(), h
+
+
+def _slabs(c, dtype, world):
+    from pycsou_amd.parallel import SlabPDS2D, run_local
+    pds = build(c, dtype, engine='fused')
+    slabs = [SlabPDS2D.from_pds(pds, None, rank=r, world=world) for r in range(world)]
+    res = run_local(slabs, pds.max_iter, pds.min_iter, pds.accuracy_threshold)
+    N = int(np.prod(c['shape']))
+    x = torch.cat([r[1] for r in res])
+    z = torch.cat([torch.cat([r[2][:r[2].numel() // 2] for r in res]),
+                   torch.cat([r[2][r[2].numel() // 2:] for r in res])])
+    assert x.numel() == N and z.numel() == 2 * N
+    ns = {r[0] for r in res}
+    assert len(ns) == 1
+    for r in res[1:]:
+        np.testing.assert_array_equal(r[3], res[0][3])  # every rank holds the same history
+    return res[0][0], x, z, res[0][3]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('name', SLAB_CASES)
+def test_slabs_match_single_gpu(name, world, dtype):
+    c = pds_case(name)
+    n1, x1, z1, h1 = _single(c, dtype)
+    n2, x2, z2, h2 = _slabs(c, dtype, world)
+    assert n2 == n1 == int(c['n_iter'])
+    assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
+    assert torch.equal(z2, z1), (z2 - z1).abs().max().item()
+    fin = np.isfinite(h1)
+    assert np.array_equal(fin, np.isfinite(h2))
+    assert np.allclose(h2[fin], h1[fin], rtol=1e-12 if dtype == np.float64 else 1e-5, atol=0)
+    tol = 1e-9 if dtype == np.float64 else 5e-5
+    assert rel(x2.cpu().numpy(), c['x']) < tol
+
+
+def test_slab_rejects_nonseparable_and_thin():
+    from pycsou_amd.parallel import SlabPDS2D
+    c = pds_case('deconv2d_l1_fwd_57x70_psf7x4')
+    pds = build(c, np.float64, engine='fused')
+    with pytest.raises(ValueError):
+        SlabPDS2D.from_pds(pds, None, rank=0, world=2)
+    c = pds_case('deconv2d_l21_fwd_64_psf15')
+    pds = build(c, np.float64, engine='fused')
+    with pytest.raises(ValueError):
+        SlabPDS2D.from_pds(pds, None, rank=0, world=8)  # 8 rows < 15-row halo
+
+
+def _c3(n0, n1, dtype):
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.build_problem(n0, n1, dtype)
+
+
+@pytest.mark.parametrize('world', [4, 7])
+def test_c3_slabs_bitwise(world):
+    """C3 workload shape (15x15 Gaussian, TV, fp32) at 700 x 512 split 4 and 7 ways
+    (uneven slabs), 30 fixed iterations."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.parallel import SlabPDS2D, run_local
+    pds = _c3(700, 512, torch.float32)
+    spec = pds._fused_spec()
+    eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    n, x1, z1, h1 = eng.run(29, 29, 0.0)
+    slabs = [SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, r, world)
+             for r in range(world)]
+    res = run_local(slabs, 29, 29, 0.0)
+    assert all(r[0] == n == 30 for r in res)
+    x2 = torch.cat([r[1] for r in res])
+    assert torch.equal(x2, x1)
+    assert np.allclose(res[0][3][1:], h1[1:], rtol=1e-5)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def test_two_process_gloo(tmp_path):
+    """Two ranks in two processes on the one GPU, gloo transport (host-staged)."""
+    name = 'deconv2d_l21_fwd_64_psf15'
+    c = pds_case(name)
+    n1, x1, z1, h1 = _single(c, np.float64)
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE='2',
+                   LOCAL_RANK='0', PYTHONPATH=ROOT)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, 'tests', 'slab_worker.py'), name,
+                                       str(tmp_path)], env=env, cwd=ROOT))
+    rcs = [p.wait(timeout=300) for p in procs]
+    assert rcs == [0, 0]
+    x = np.load(tmp_path / 'x.npy')
+    h = np.load(tmp_path / 'hist.npy')
+    assert int(np.load(tmp_path / 'n.npy')) == n1
+    np.testing.assert_array_equal(x, x1.cpu().numpy())
+    fin = np.isfinite(h1)
+    assert np.allclose(h[fin], h1[fin], rtol=1e-12)
