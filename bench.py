@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 METRIC = 'PDS iters/sec on 4096² TV-deconv; achieved HBM GB/s vs roofline at 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+TRAFFIC_JSON = 'profiles/r1_traffic.json'  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the step kernel (tools/prof_run.sh)
 
 
 def phantom(shape, n_rect, seed):
@@ -185,6 +186,11 @@ def main():
         ms = res['ms_per_step']
         value = world / (ms * 1e-3)  # 4096^2-image iterations per second, whole job
         achieved = alg_bytes / (res['kernel_ms'] * 1e-3) / 1e9
+        traffic, tsrc = None, None
+        tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON)
+        if os.path.exists(tpath) and dtype == torch.float32 and n == 4096:
+            traffic = round(json.load(open(tpath))['traffic_bytes'])  # PMC FETCH/WRITE per launch (corrected)
+            tsrc = TRAFFIC_JSON
         out = {
             'metric': METRIC, 'value': round(value, 3), 'unit': 'it/s', 'n_gpus': world, 'steps': K, 'warmup': W,
             'ms_per_step': round(ms, 5), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
@@ -197,7 +203,7 @@ def main():
                                       'slab engine: per-iteration RCCL all-gather of 4 sums + halo exchange'),
                        'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,
                          'kernel': 'pcs_pds2d_step (k_pds2d<float,2,7,32>)',
                          'kernel_ms': round(res['kernel_ms'], 5), 'alg_bytes_per_launch': alg_bytes},
             'iteration_GBps': round(alg_bytes / (ms * 1e-3) / 1e9, 1),

@@ -131,7 +131,8 @@ int pcs_reduce(int dtype, int kind, const void* x, const void* y, int64_t n, dou
  *   z'  = rho z_t + (1-rho) z ;  x' = rho x_t + (1-rho) x
  * plus per-block partials of ||x-x'||^2, ||x||^2, ||z-z'||^2, ||z||^2.
  * Slab form: the local arrays hold rows [row0 - halo, row0 + rows + halo) of a
- * global n0 x n1 image (halo rows of x: pcs_pds2d_halo_x, of z: 2, of y: halo_x/2+1). */
+ * global n0 x n1 image (halo rows of x >= pcs_pds2d_halo_x(half), of each z component >= 1,
+ * of y >= (pcs_pds2d_halo_x(half) - 1)/2 + 1); only the slab's own rows of xn/zn are written. */
 typedef struct {
   int dtype;          /* PCS_F32 / PCS_F64 */
   int fkind;          /* PCS_F_* */
