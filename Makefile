@@ -21,3 +21,10 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
+
+# Diagnostic build with s_memtime stamps in the march kernel (tools/march_stamps.py)
+STAMP_LIB := pycsou_amd/lib/diag/libpycsou_hip.so
+stamps: $(SRC) $(HDR)
+	@mkdir -p pycsou_amd/lib/diag
+	$(HIPCC) $(FLAGS) -DPCS_STAMPS -shared -o $(STAMP_LIB) $(SRC)
+.PHONY: stamps

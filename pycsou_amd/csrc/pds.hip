@@ -8,7 +8,7 @@
 // with F = 1/2 ||Conv x - y||^2 (Conv separable, centred taps), 1/2 ||x - y||^2, 0, or a
 // precomputed gradient buffer; K = Gradient(kind='forward'); H = lam*L1 / lam*L21 (pixel
 // groups); G = Null / NonNegativeOrthant / Segment.  The tile kernel is in pds_tile.hpp.
-#include "pds_tile.hpp"
+#include "pds_march.hpp"
 
 namespace pcs {
 
@@ -99,16 +99,14 @@ static int tier_for(int half) {
 
 static bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
 
-template <typename T, int FK, int H>
-static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
-  constexpr int TH = Tile<T>::TH, NT = Tile<T>::NT;
-  const int tiles_x = (int)((a->n1 + 63) / 64);
-  const int tiles_y = (int)((a->rows + TH - 1) / TH);
-  const int64_t ntiles = (int64_t)tiles_x * tiles_y;
-  if (ntiles > 0x7fffffff) return PCS_EUNSUPPORTED;
+static Slab make_slab(const pcs_pds2d_args* a) {
   const int vec = (a->n1 % 4 == 0) && aligned16(a->x) && aligned16(a->xn) && aligned16(a->z) && aligned16(a->zn) &&
                   aligned16(a->y) && aligned16(a->gbuf);
-  Slab s{a->n0, a->n1, a->row0, a->rows, a->halo_x, a->halo_y, a->halo_z, vec};
+  return Slab{a->n0, a->n1, a->row0, a->rows, a->halo_x, a->halo_y, a->halo_z, vec};
+}
+
+template <typename T>
+static Params<T> make_params(const pcs_pds2d_args* a) {
   Params<T> P;
   P.tau = (T)a->tau;
   P.sigma = (T)a->sigma;
@@ -124,15 +122,118 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   P.unit1 = a->step1 == 1.0;
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
+  return P;
+}
+
+template <typename T, int FK, int H>
+static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
+  constexpr int TH = Tile<T>::TH, NT = Tile<T>::NT;
+  const int tiles_x = (int)((a->n1 + 63) / 64);
+  const int tiles_y = (int)((a->rows + TH - 1) / TH);
+  const int64_t ntiles = (int64_t)tiles_x * tiles_y;
+  if (ntiles > 0x7fffffff) return PCS_EUNSUPPORTED;
+  const Slab s = make_slab(a);
+  const Params<T> P = make_params<T>(a);
   k_pds2d<T, FK, H, TH, NT><<<(unsigned)ntiles, NT, 0, st>>>(
       (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->y, (const T*)a->gbuf, (const T*)a->taps0,
       (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, tiles_x,
-      (int)ntiles);
+      (int)ntiles, tiles_x, 0);
+  return launch_status();
+}
+
+// ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel on the column-interior
+// strips, the tile kernel on the boundary strips, then the reduction (+ loop control)
+constexpr int kMarchNT = 256;
+
+struct MarchPlan {
+  int tiles_x, bl, br;           // 64-column strips; boundary strips on the left / right
+  int mstrips, seg_len, ntasks;  // march kernel: interior strips, rows per task, tasks
+  int btiles;                    // tile kernel: tiles on the boundary strips
+};
+
+// resident workgroups of the march kernel on the whole device (queried once)
+template <int H>
+static int march_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_march<float, H, kMarchNT>, kMarchNT, 0) !=
+            hipSuccess ||
+        nb < 1)
+      nb = 3;
+    (void)hipGetLastError();
+    slots = cus * nb;
+  }
+  return slots;
+}
+
+// One march task = one interior 64-column strip x one row segment; as many segments as fill
+// the device in one wave of resident workgroups (equal segments: no tail).  False when no
+// strip is column-interior (narrow images) -> tile kernel only.
+template <int H>
+static bool march_plan(const pcs_pds2d_args* a, MarchPlan* p) {
+  using M = March<H>;
+  constexpr int TS = M::TS;
+  p->tiles_x = (int)((a->n1 + M::TW - 1) / M::TW);
+  if (p->tiles_x < 2) return false;  // narrow images: the tile kernel
+  p->bl = p->br = 0;                 // every strip marches (edge columns clamp + zero)
+  p->mstrips = p->tiles_x;
+  const int64_t steps = (a->rows + TS - 1) / TS;
+  int64_t nseg = march_slots<H>() / p->mstrips;
+  nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
+  const int64_t steps_per = (steps + nseg - 1) / nseg;
+  p->seg_len = (int)(steps_per * TS);
+  nseg = (a->rows + p->seg_len - 1) / p->seg_len;
+  p->ntasks = (int)(p->mstrips * nseg);
+  p->btiles = 0;
+  return true;
+}
+
+static bool use_march(const pcs_pds2d_args* a) {
+  static int disabled = -1;  // PCS_NO_MARCH=1: diagnostics, force the tile kernel
+  if (disabled < 0) disabled = getenv("PCS_NO_MARCH") != nullptr;
+  if (disabled) return false;
+  const int t = tier_for(a->half);
+  if (a->dtype != PCS_F32 || a->fkind != PCS_F_SEPCONV || (t != 3 && t != 7) || !make_slab(a).vec) return false;
+  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
+                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax + 64) * (a->n1 + 64) < (1LL << 31))) return false;
+  MarchPlan p;
+  return t == 3 ? march_plan<3>(a, &p) : march_plan<7>(a, &p);
+}
+
+template <int H>
+static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
+  MarchPlan p;
+  if (!march_plan<H>(a, &p)) return PCS_EINVAL;
+  const Slab s64 = make_slab(a);
+  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
+  const Params<float> P = make_params<float>(a);
+  k_pds2d_march<float, H, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
+      (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
+      (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials,
+      (const Ctrl*)a->ctrl, p.bl, p.mstrips, p.seg_len, p.ntasks);
+  if (p.btiles > 0) {
+    constexpr int TH = Tile<float>::TH, NT = Tile<float>::NT;
+    const int nb = p.bl + p.br;
+    k_pds2d<float, PCS_F_SEPCONV, H, TH, NT><<<(unsigned)p.btiles, NT, 0, st>>>(
+        (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y, nullptr,
+        (const float*)a->taps0, (const float*)a->taps1, a->half, s64, P, a->hkind, a->gkind,
+        a->partials + 4 * (int64_t)p.ntasks, (Ctrl*)a->ctrl, nullptr, nullptr, nb, p.btiles, p.bl,
+        p.tiles_x - nb);
+  }
+  if (a->hist != nullptr)
+    k_reduce_finalize<<<1, kRedThreads, 0, st>>>(a->partials, (int64_t)p.ntasks + p.btiles, (Ctrl*)a->ctrl,
+                                                  a->hist);
   return launch_status();
 }
 
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
+  if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, st) : launch_march<7>(a, st);
   switch (a->fkind) {
     case PCS_F_NULL: return launch_pds2d<T, PCS_F_NULL, 0>(a, st);
     case PCS_F_DENOISE: return launch_pds2d<T, PCS_F_DENOISE, 0>(a, st);
@@ -164,7 +265,13 @@ extern "C" {
 int pcs_pds2d_halo_x(int half) { return 1 + 2 * tier_for(half < 0 ? 0 : half); }
 
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
-  if (!a) return -1;
+  if (!a || a->rows < 1 || a->n1 < 1) return -1;
+  if (use_march(a)) {
+    MarchPlan p;
+    if (tier_for(a->half) == 3) march_plan<3>(a, &p);
+    else march_plan<7>(a, &p);
+    return (int64_t)p.ntasks + p.btiles;
+  }
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);
 }
@@ -197,6 +304,15 @@ int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
 }
 
 int64_t pcs_ctrl_bytes(void) { return 64; }
+
+#ifdef PCS_STAMPS
+// diagnostic build only: copy the march kernel's per-segment stamp totals to the host
+int pcs_debug_stamps(void* host, int64_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pcs_stamps), (size_t)bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : PCS_ELAUNCH;
+}
+#endif
 
 int pcs_ctrl_init2(void* ctrl, int min_iter, int max_iter, double thr, int has_dual, int hist_len, hipStream_t st) {
   if (!ctrl || hist_len < 2) return PCS_EINVAL;

@@ -472,7 +472,8 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
                                                const T* __restrict__ gbuf, const T* __restrict__ taps0,
                                                const T* __restrict__ taps1, int half, Slab s, Params<T> P, int hk,
                                                int gk, double* __restrict__ partials, Ctrl* ctrl,
-                                               double* hist, void* ws, int tiles_x, int ntiles) {
+                                               double* hist, void* ws, int tiles_x, int ntiles, int bl,
+                                               int tx_shift) {
   constexpr bool CONV = (FK == PCS_F_SEPCONV);
   constexpr int TW = 64;
   constexpr int H4 = RU4<H>::value;
@@ -494,7 +495,8 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
     const int b = blockIdx.x, q = ntiles / 8, r = ntiles % 8, xcd = b % 8, k = b / 8;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int ty = tile / tiles_x, txs = tile - ty * tiles_x;
+  const int tx = txs < bl ? txs : txs + tx_shift;  // strip subset: [0, bl) and the right-most strips
   const int64_t t0 = (int64_t)ty * TH, c0 = (int64_t)tx * TW;
 
   T w0[2 * H + 1], w1[2 * H + 1];
