@@ -200,7 +200,8 @@ static bool use_march(const pcs_pds2d_args* a) {
   if (a->dtype != PCS_F32 || a->fkind != PCS_F_SEPCONV || (t != 3 && t != 7) || !make_slab(a).vec) return false;
   const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
                                              : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
-  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax + 64) * (a->n1 + 64) < (1LL << 31))) return false;
+  // 32-bit indexing and buffer views of at most 2^30 bytes (pds_march.hpp kOOB)
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
   MarchPlan p;
   return t == 3 ? march_plan<3>(a, &p) : march_plan<7>(a, &p);
 }
@@ -215,7 +216,7 @@ static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
   k_pds2d_march<float, H, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials,
-      (const Ctrl*)a->ctrl, p.bl, p.mstrips, p.seg_len, p.ntasks);
+      (Ctrl*)a->ctrl, p.btiles > 0 ? nullptr : a->hist, a->ws, p.bl, p.mstrips, p.seg_len, p.ntasks);
   if (p.btiles > 0) {
     constexpr int TH = Tile<float>::TH, NT = Tile<float>::NT;
     const int nb = p.bl + p.br;
@@ -225,7 +226,7 @@ static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
         a->partials + 4 * (int64_t)p.ntasks, (Ctrl*)a->ctrl, nullptr, nullptr, nb, p.btiles, p.bl,
         p.tiles_x - nb);
   }
-  if (a->hist != nullptr)
+  if (a->hist != nullptr && p.btiles > 0)
     k_reduce_finalize<<<1, kRedThreads, 0, st>>>(a->partials, (int64_t)p.ntasks + p.btiles, (Ctrl*)a->ctrl,
                                                   a->hist);
   return launch_status();

@@ -35,9 +35,11 @@ struct March {
   static constexpr int WG = TW + 4, GG = WG / 4;          // U cols [c0, c0 + WG)
   static constexpr int WR = WG + 2 * H4, GR = WR / 4;     // residual cols [c0 - H4, c0 + WG + H4)
   static constexpr int WX = WG + 4 * H4, GX = WX / 4;     // x / A cols [c0 - 2 H4, c0 + WG + 2 H4)
-  static constexpr int RR1 = 2, NI1 = (TS / RR1) * GX;    // P1 items: 2 rows x 1 group
-  static constexpr int NG2 = 2, NPR2 = (GR + NG2 - 1) / NG2, NI2 = TS * NPR2;  // P2 items: 1 row x 2 groups
-  static constexpr int RR3 = 2, NQ3 = (UR + RR3 - 1) / RR3, NI3 = NQ3 * GR;    // P3 items: 2 rows x 1 group
+  // P1 items: RR1 rows x 1 group, 32 lanes per row block (lanes past the row's groups redo its
+  // last group) so every 16-lane ds_read_b128 group reads 16 distinct slots of one row
+  static constexpr int RR1 = 2, NI1 = (TS / RR1) * 32;                         // P1
+  static constexpr int NG2 = 2, NPR2 = (GR + NG2 - 1) / NG2, NI2 = TS * NPR2;  // P2: 1 row x 2 groups
+  static constexpr int RR3 = 2, NQ3 = (UR + RR3 - 1) / RR3, NI3 = NQ3 * GR;    // P3: 2 rows x 1 group
   static constexpr int NI5 = UR * GG, NI6 = TS * (TW / 4);
   static constexpr int NZ0 = (UR + 1) * GG, NZ1 = UR * (GG + 1);
   static constexpr int NXN = TS * GX;                       // new x rows per step
@@ -54,6 +56,7 @@ struct March {
   static constexpr int SZ = O_Z1 + SZ_Z1;
   static_assert(TS + 2 * H + 1 <= RING, "x ring holds rows [a+1, a+TS+2H+1) plus the next chunk's rows");
   static_assert(TS >= 2 * H + 1 && 2 * TS <= RING, "residual ring holds two chunks covering [a - H, a + TS + H]");
+  static_assert(GX <= 32 && GR <= 32, "a row block fits 32 lanes");
 };
 
 // Diagnostic build only (-DPCS_STAMPS): per-segment s_memtime totals of waves 0 and 3 of
@@ -288,7 +291,7 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   auto p1 = [&](int cs) {
     if (PCS_WAVE_ON(0, M::NI1)) {
       const int e = PCS_ITEM(0, M::NI1);
-      const int q = e / GX, g = e - (e / GX) * GX;
+      const int q = e >> 5, g = min(e & 31, GX - 1);
       const int sl = (cs + q * RR1 - H - xb) & 31;
       G4<T> acc[RR1];
       vpass<T, H, RR1, true, 4>(XR, WX, sl, 4 * g, w0, acc);
@@ -556,16 +559,17 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
 }
 
 // One block per task (64-column strip x row segment, strips strip0 .. strip0 + tiles_x - 1);
-// writes one partial per task -- the reduction follows in the same stream.
+// with `hist` the last workgroups also reduce the partials and run the loop control.
 template <typename T, int H, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_pds2d_march(
     const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
     const T* __restrict__ y, const T* __restrict__ taps0, const T* __restrict__ taps1, int half, Slab32 s,
-    Params<T> P, int hk, int gk, double* __restrict__ partials, const Ctrl* ctrl, int strip0, int tiles_x,
-    int seg_len, int ntasks) {
+    Params<T> P, int hk, int gk, double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws, int strip0,
+    int tiles_x, int seg_len, int ntasks) {
   using M = March<H>;
   __shared__ __attribute__((aligned(16))) T sm[M::SZ];
   __shared__ double red[4 * (NT / 64)];
+  __shared__ int flag[2];
   if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
 
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
@@ -589,9 +593,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   march_task<T, H, NT>(x, xn, z, zn, y, w0, w1, s, P, hk, gk, s0, s1, c0, sm, part);
   block_sum<4>(part, red);
-  if (threadIdx.x == 0) {
+  if (hist != nullptr) {  // single launch per iteration: the last workgroups reduce + finalize
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
+  } else if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)task * 4 + k] = part[k];
+    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
   }
 }
 
