@@ -158,6 +158,32 @@ int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
 int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a);
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
 
+/* One fused PrimalDualSplitting.update_iterand + update_diagnostics for 3-D volumes
+ * (pycsou/opt/proxalgs.py:343-394), K = Gradient(kind='forward') in 3-D
+ * (pycsou/linop/diff.py:777-882): the same update as pcs_pds2d_step with three gradient
+ * components (z = [D0 x; D1 x; D2 x]) and grad F taken from `g`:
+ *   fkind PCS_F_NULL: 0;  PCS_F_DENOISE: x - g (g holds y);  PCS_F_GRADBUF: g.
+ * Volume n0 x n1 x n2 (C order, n2 % 4 == 0); slab form as in 2-D along axis 0: the local
+ * arrays hold planes [plane0 - halo, plane0 + planes + halo); `g` must supply planes
+ * [0, planes] (one past the slab) when planes < n0. */
+typedef struct {
+  int dtype, fkind, hkind, gkind;
+  int64_t n0, n1, n2;
+  int64_t plane0, planes;
+  int halo_x, halo_z, halo_g;
+  int pad;
+  double tau, sigma, rho, lam, step0, step1, step2, seg_a, seg_b;
+  const void* x; void* xn; const void* z; void* zn; const void* g;
+  double* partials;       /* [nblocks][4] */
+  void* ctrl;             /* device control block; NULL = always run */
+  double* hist;           /* non-NULL: in-launch reduce + loop control (single GPU) */
+  void* ws;               /* with hist: pcs_pds3d_ws_bytes() bytes, zeroed once */
+} pcs_pds3d_args;
+
+int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a);
+int64_t pcs_pds3d_ws_bytes(const pcs_pds3d_args* a);
+int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t stream);
+
 /* Device control block for the hipGraph-captured loop:
  * int32 [0]=it (next iteration), [1]=stopped, [2]=min_iter, [3]=max_iter, [4]=has_dual,
  * [5]=hist_len; double at byte 32: accuracy_threshold.

@@ -38,6 +38,17 @@ class PdsArgs(ctypes.Structure):
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
 
 
+class Pds3Args(ctypes.Structure):
+    """Mirror of pcs_pds3d_args."""
+    _fields_ = [('dtype', _c_int), ('fkind', _c_int), ('hkind', _c_int), ('gkind', _c_int),
+                ('n0', _c_i64), ('n1', _c_i64), ('n2', _c_i64), ('plane0', _c_i64), ('planes', _c_i64),
+                ('halo_x', _c_int), ('halo_z', _c_int), ('halo_g', _c_int), ('pad', _c_int),
+                ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
+                ('step0', _c_dbl), ('step1', _c_dbl), ('step2', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
+                ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('g', _vp),
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     'pcs_abi_version': (_c_int, []),
@@ -67,6 +78,9 @@ _SIGS = {
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
+    'pcs_pds3d_nblocks': (_c_i64, [ctypes.POINTER(Pds3Args)]),
+    'pcs_pds3d_ws_bytes': (_c_i64, [ctypes.POINTER(Pds3Args)]),
+    'pcs_pds3d_step': (_c_int, [ctypes.POINTER(Pds3Args), _vp]),
     'pcs_ctrl_bytes': (_c_i64, []),
     'pcs_ctrl_init': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _vp]),
     'pcs_ctrl_init2': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _c_int, _vp]),

@@ -1,0 +1,435 @@
+// Fused PrimalDualSplitting update for 3-D volumes (K = Gradient(kind='forward') in 3-D).
+//
+//   x_t = prox_G((x - tau g) - tau K^T z)        g = grad F (precomputed buffer, x - y, or 0)
+//   u   = 2 x_t - x
+//   z_t = H.fenchel_prox(z + sigma K u, sigma)   H = lam*L1 or lam*L21 over the 3 gradient components
+//   z'  = rho z_t + (1-rho) z ;  x' = rho x_t + (1-rho) x
+// plus the four norm partials of update_diagnostics -- pycsou/opt/proxalgs.py:343-394 with
+// K from pycsou/linop/diff.py:777-882 (PyLops Gradient: VStack of forward FirstDerivatives,
+// last sample 0; adjoint accumulated in axis order).
+//
+// Layout: C-order volume (n0 planes of n1 x n2); z = [D0 x; D1 x; D2 x], each component with
+// the same (halo'd) plane layout.  A workgroup owns an 8 x 64 in-plane tile and marches down a
+// segment of planes: at plane p it lands z(p) in LDS, computes x_t / u on the tile plus one
+// row / one 4-group of halo (u of plane p in a 2-plane LDS ring), writes x'(p), and then
+// z'(p-1), whose axis-0 difference needs u(p).  Loads for plane p+1 are issued before plane
+// p's work.  Every load goes through a buffer descriptor of ONE plane (num_records = 0 for a
+// plane outside the image or the stored slab, so those read 0) with in-plane rows / columns
+// outside the image pushed past the range: no branches, no selects.
+#include "pds_march.hpp"
+
+namespace pcs {
+
+template <typename T>
+struct P3 {
+  T tau, sigma, inv_sigma, rho, omr, t_h, inv_t_h, inv_step[3], seg_a, seg_b;
+  int unit[3];
+};
+
+struct Vol {
+  int n0, n1, n2, plane0, planes, hx, hz, hg;
+  uint32_t pitch1, plane_bytes;  // bytes per row (n2 * elem), per plane
+};
+
+template <typename T>
+__device__ __forceinline__ G4<T> bload(Rsrc r, uint32_t off);
+template <>
+__device__ __forceinline__ G4<float> bload<float>(Rsrc r, uint32_t off) {
+  return bload4(r, off);
+}
+template <>
+__device__ __forceinline__ G4<double> bload<double>(Rsrc r, uint32_t off) {
+  const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off + 16), 0, 0);
+  G4<double> g;
+  g.v[0] = __hiloint2double((int)a[1], (int)a[0]);
+  g.v[1] = __hiloint2double((int)a[3], (int)a[2]);
+  g.v[2] = __hiloint2double((int)b[1], (int)b[0]);
+  g.v[3] = __hiloint2double((int)b[3], (int)b[2]);
+  return g;
+}
+
+// descriptor of local plane p of an array stored with `halo` planes on each side (0 records
+// when the plane is outside the image or the stored planes)
+template <typename T>
+__device__ __forceinline__ Rsrc plane_rsrc(const T* base, const Vol& v, int halo, int p) {
+  const int gp = v.plane0 + p;
+  const bool ok = gp >= 0 && gp < v.n0 && p >= -halo && p < v.planes + halo;
+  const T* pl = base + (int64_t)(ok ? p + halo : 0) * v.n1 * v.n2;
+  return rsrc_of(pl, ok ? v.plane_bytes : 0u);
+}
+// in-plane byte offset of (row i1, column i2) -- kOOB parts outside the image
+template <typename T>
+__device__ __forceinline__ uint32_t inplane(const Vol& v, int i1, int i2) {
+  const uint32_t ro = ((unsigned)i1 < (unsigned)v.n1) ? (uint32_t)i1 * v.pitch1 : kOOB;
+  const uint32_t co = ((unsigned)i2 < (unsigned)v.n2) ? (uint32_t)i2 * (uint32_t)sizeof(T) : kOOB;
+  return ro + co;
+}
+
+// one element (odd widths: n2 % 4 != 0)
+template <typename T>
+__device__ __forceinline__ T bload1(Rsrc r, uint32_t off);
+template <>
+__device__ __forceinline__ float bload1<float>(Rsrc r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+template <>
+__device__ __forceinline__ double bload1<double>(Rsrc r, uint32_t off) {
+  const auto a = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return __hiloint2double((int)a[1], (int)a[0]);
+}
+
+// In-plane offsets of a 4-column group: one 16-B access when n2 % 4 == 0 (VEC: groups are
+// wholly inside or outside the image), four element accesses otherwise.
+template <typename T, bool VEC>
+struct GOff {
+  uint32_t o[VEC ? 1 : 4];
+};
+template <typename T, bool VEC>
+__device__ __forceinline__ GOff<T, VEC> goff(const Vol& v, int i1, int c) {
+  GOff<T, VEC> g;
+#pragma unroll
+  for (int m = 0; m < (VEC ? 1 : 4); ++m) g.o[m] = inplane<T>(v, i1, c + m);
+  return g;
+}
+template <typename T, bool VEC>
+__device__ __forceinline__ G4<T> gload(Rsrc r, const GOff<T, VEC>& g) {
+  if constexpr (VEC) {
+    return bload<T>(r, g.o[0]);
+  } else {
+    G4<T> out;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) out.v[m] = bload1<T>(r, g.o[m]);
+    return out;
+  }
+}
+// store the in-image elements of a group (row i1 inside the image)
+template <typename T, bool VEC>
+__device__ __forceinline__ void gstore(T* p, const G4<T>& g, int c, int n2) {
+  if constexpr (VEC) {
+    st4(p, g);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (c + m < n2) p[m] = g.v[m];
+  }
+}
+
+constexpr int k3T1 = 8, k3TW = 64, k3NT = 256;
+
+template <typename T, int FK, bool VEC>
+__global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
+                                                 const T* __restrict__ z, T* __restrict__ zn,
+                                                 const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk,
+                                                 double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
+                                                 int tiles1, int tiles2, int seg_len, int ntasks) {
+  constexpr int T1 = k3T1, TW = k3TW, NT = k3NT;
+  constexpr int UR = T1 + 1, WG = TW + 4, GG = WG / 4;
+  constexpr int NU = UR * GG;                 // U items (x_t / u), 153
+  constexpr int NZ = T1 * (TW / 4);           // z' items, 128
+  constexpr int NZ1 = (T1 + 2) * GG;          // z1 rows [r1-1, r1+T1]
+  constexpr int NZ2 = UR * (GG + 1);          // z2 cols [c2-4, c2+WG)
+  constexpr int SZU = UR * WG, SZ0 = UR * WG, SZ1 = (T1 + 2) * WG, SZ2 = UR * (WG + 4);
+  static_assert(NU <= NT && NZ <= NT && NZ1 <= NT && NZ2 <= NT, "one item per thread");
+  __shared__ __attribute__((aligned(16))) T U[2][SZU];
+  __shared__ __attribute__((aligned(16))) T Z0[2][SZ0];
+  __shared__ __attribute__((aligned(16))) T Z1[2][SZ1];
+  __shared__ __attribute__((aligned(16))) T Z2[2][SZ2];
+  __shared__ double red[4 * (NT / 64)];
+  __shared__ int flag[2];
+  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
+
+  int task;
+  {  // XCD-aware bijective remap: consecutive tasks (neighbouring tiles of a segment) share an XCD
+    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int per_plane = tiles1 * tiles2;
+  const int seg = task / per_plane, t12 = task - seg * per_plane;
+  const int ty = t12 / tiles2, tx = t12 - ty * tiles2;
+  const int r1 = ty * T1, c2 = tx * TW;
+  const int p_start = seg * seg_len, p_end = min(p_start + seg_len, v.planes);  // own planes [p_start, p_end)
+  const int tid = threadIdx.x;
+  const int64_t zstride = (int64_t)(v.planes + 2 * v.hz) * v.n1 * v.n2;
+  const int64_t pl = (int64_t)v.n1 * v.n2;
+
+  // fixed per-thread item geometry
+  const int ue = min(tid, NU - 1), ui = ue / GG, ug = ue - (ue / GG) * GG;  // U item: row ui, group ug
+  const bool u_real = tid < NU;
+  const int ze = min(tid, NZ - 1), zi = ze / (TW / 4), zg = ze - (ze / (TW / 4)) * (TW / 4);
+  const int e1 = min(tid, NZ1 - 1), e1r = e1 / GG, e1g = e1 - (e1 / GG) * GG;
+  const int e2 = min(tid, NZ2 - 1), e2r = e2 / (GG + 1), e2g = e2 - (e2 / (GG + 1)) * (GG + 1);
+  const GOff<T, VEC> off_u = goff<T, VEC>(v, r1 + ui, c2 + 4 * ug);
+  const GOff<T, VEC> off_z1 = goff<T, VEC>(v, r1 - 1 + e1r, c2 + 4 * e1g);
+  const GOff<T, VEC> off_z2 = goff<T, VEC>(v, r1 + e2r, c2 - 4 + 4 * e2g);
+  // column flags (loop-invariant): U item inside the image / on the last 4-group; z' item likewise
+  const int i1u = r1 + ui, c_u = c2 + 4 * ug, i1z = r1 + zi, c_z = c2 + 4 * zg;
+  // bits: 0 row in image, 1 group starts in image, 2 group is the last one, 3 last row; 4-7 the
+  // same for the z' item
+  const int flags = ((i1u < v.n1) ? 1 : 0) | ((c_u < v.n2) ? 2 : 0) | ((c_u == v.n2 - 4) ? 4 : 0) |
+                    ((i1u == v.n1 - 1) ? 8 : 0) | ((i1z < v.n1) ? 16 : 0) | ((c_z < v.n2) ? 32 : 0) |
+                    ((c_z == v.n2 - 4) ? 64 : 0) | ((i1z == v.n1 - 1) ? 128 : 0);
+
+  G4<T> xr, gr, z0r, z1r, z2r;
+  auto prefetch = [&](int p) {
+    const Rsrc rx = plane_rsrc(x, v, v.hx, p), rz0 = plane_rsrc(z, v, v.hz, p),
+               rz1 = plane_rsrc(z + zstride, v, v.hz, p), rz2 = plane_rsrc(z + 2 * zstride, v, v.hz, p);
+    xr = gload<T, VEC>(rx, off_u);
+    if constexpr (FK != PCS_F_NULL) gr = gload<T, VEC>(plane_rsrc(g, v, v.hg, p), off_u);
+    z0r = gload<T, VEC>(rz0, off_u);
+    z1r = gload<T, VEC>(rz1, off_z1);
+    z2r = gload<T, VEC>(rz2, off_z2);
+  };
+  auto land = [&](int slot) {
+    if (tid < NU) st4(&Z0[slot][ui * WG + 4 * ug], z0r);
+    if (tid < NZ1) st4(&Z1[slot][e1r * WG + 4 * e1g], z1r);
+    if (tid < NZ2) st4(&Z2[slot][e2r * (WG + 4) + 4 * e2g], z2r);
+  };
+
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  // prologue: z0 of plane p_start - 1 (for D0^T z0 at p_start), then plane p_start's data
+  {
+    const Rsrc rz0 = plane_rsrc(z, v, v.hz, p_start - 1);
+    const G4<T> zp = gload<T, VEC>(rz0, off_u);
+    if (tid < NU) st4(&Z0[(p_start - 1) & 1][ui * WG + 4 * ug], zp);
+  }
+  prefetch(p_start);
+  for (int p = p_start; p <= p_end; ++p) {
+    const int slot = p & 1, prev = slot ^ 1;
+    const int gp = v.plane0 + p;
+    lds_barrier();  // plane p-1's z' items are done with U[slot], Z*[slot]
+    const G4<T> xv4 = xr;
+    G4<T> gv4;
+    if constexpr (FK != PCS_F_NULL) gv4 = gr;
+    land(slot);
+    if (p < p_end) prefetch(p + 1);
+    lds_barrier();
+    const int fl = launder(flags);
+    // ---- U items: x_t, u on rows [r1, r1 + T1], cols [c2, c2 + WG) of plane p; x' on own cells
+    {  // every thread runs an item (surplus threads redo the last one; only real items store)
+      const G4<T> zb = lds4(&Z0[slot][ui * WG + 4 * ug]);         // z0(p)
+      const G4<T> za = lds4(&Z0[prev][ui * WG + 4 * ug]);         // z0(p-1)
+      const G4<T> z1a = lds4(&Z1[slot][ui * WG + 4 * ug]);        // z1(p, i1-1)
+      const G4<T> z1b = lds4(&Z1[slot][(ui + 1) * WG + 4 * ug]);  // z1(p, i1)
+      const G4<T> z2a = lds4(&Z2[slot][ui * (WG + 4) + 4 * ug]);  // z2(p, c-4 .. c-1)
+      const G4<T> z2b = lds4(&Z2[slot][ui * (WG + 4) + 4 * ug + 4]);
+      const bool rin = fl & 1, gin = fl & 2, glast = fl & 4, rlast = fl & 8;
+      const bool p_first = gp <= 0, p_last = gp >= v.n0 - 1;
+      const bool in = rin && gin && gp >= 0 && gp < v.n0 && p <= v.planes;
+      const bool own = in && u_real && ui < T1 && ug < TW / 4 && p < p_end;
+      G4<T> uo, xo;
+      T sdx = T(0), sx = T(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const T xv = xv4.v[m];
+        T gf;
+        if constexpr (FK == PCS_F_NULL) gf = T(0);
+        else if constexpr (FK == PCS_F_DENOISE) gf = xv - gv4.v[m];
+        else gf = gv4.v[m];
+        // K^T z, VStack order: ((0 + D0^T z0) + D1^T z1) + D2^T z2; neighbours outside the
+        // image load as 0, the last sample of each forward difference is not used
+        T d0 = p_first ? T(0) : za.v[m];
+        if (!p_last) d0 -= zb.v[m];
+        T d1 = z1a.v[m];
+        if (!rlast) d1 -= z1b.v[m];
+        const T z2l = (m == 0) ? z2a.v[3] : z2b.v[m - 1];
+        const bool lastc = VEC ? (m == 3 && glast) : (c_u + m == v.n2 - 1);
+        const bool cm = VEC ? true : (c_u + m < v.n2);  // element inside the image (group known in)
+        const T d2 = z2l - (lastc ? T(0) : z2b.v[m]);
+        const T a0 = P.unit[0] ? d0 : d0 * P.inv_step[0];
+        const T a1 = P.unit[1] ? d1 : d1 * P.inv_step[1];
+        const T a2 = P.unit[2] ? d2 : d2 * P.inv_step[2];
+        const T xt = prox_g((xv - P.tau * gf) - P.tau * ((a0 + a1) + a2), gk, P.seg_a, P.seg_b);
+        uo.v[m] = (in && cm) ? (T(2) * xt - xv) : T(0);
+        const T xnew = P.rho * xt + P.omr * xv;
+        xo.v[m] = xnew;
+        const T dx = xv - xnew;
+        sdx += cm ? dx * dx : T(0);
+        sx += cm ? xv * xv : T(0);
+      }
+      if (own) {
+        part[0] += (double)sdx;
+        part[1] += (double)sx;
+        gstore<T, VEC>(xn + (int64_t)(p + v.hx) * pl + (int64_t)i1u * v.n2 + c_u, xo, c_u, v.n2);
+      }
+      if (tid < NU) st4(&U[slot][ui * WG + 4 * ug], uo);
+    }
+    lds_barrier();
+    // ---- z' items for plane p - 1 (own tile)
+    if (p > p_start && tid < NZ) {
+      const int q = p - 1, gq = gp - 1;
+      const bool rin = fl & 16, gin = fl & 32, glast = fl & 64, rlast = fl & 128;
+      const bool own = rin && gin && gq < v.n0;
+      const G4<T> uc = lds4(&U[prev][zi * WG + 4 * zg]);
+      const G4<T> un = lds4(&U[prev][zi * WG + 4 * zg + 4]);
+      const G4<T> ud = lds4(&U[prev][(zi + 1) * WG + 4 * zg]);
+      const G4<T> up = lds4(&U[slot][zi * WG + 4 * zg]);  // u(p)
+      const G4<T> zv0 = lds4(&Z0[prev][zi * WG + 4 * zg]);
+      const G4<T> zv1 = lds4(&Z1[prev][(zi + 1) * WG + 4 * zg]);
+      const G4<T> zv2 = lds4(&Z2[prev][zi * (WG + 4) + 4 * zg + 4]);
+      const bool q_last = gq >= v.n0 - 1;
+      G4<T> o0, o1, o2;
+      T sdz = T(0), sz = T(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const T uright = (m < 3) ? uc.v[m + 1] : un.v[0];
+        const T d0 = q_last ? T(0) : (up.v[m] - uc.v[m]);
+        const T d1 = rlast ? T(0) : (ud.v[m] - uc.v[m]);
+        const bool lastc = VEC ? (m == 3 && glast) : (c_z + m == v.n2 - 1);
+        const bool cm = VEC ? true : (c_z + m < v.n2);
+        const T d2 = lastc ? T(0) : (uright - uc.v[m]);
+        const T k0 = P.unit[0] ? d0 : d0 * P.inv_step[0];
+        const T k1 = P.unit[1] ? d1 : d1 * P.inv_step[1];
+        const T k2 = P.unit[2] ? d2 : d2 * P.inv_step[2];
+        const T w0 = zv0.v[m] + P.sigma * k0, w1 = zv1.v[m] + P.sigma * k1, w2 = zv2.v[m] + P.sigma * k2;
+        const T v0 = w0 * P.inv_sigma, v1 = w1 * P.inv_sigma, v2 = w2 * P.inv_sigma;
+        T t0, t1, t2;
+        if (hk == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
+          T f = T(1) - P.t_h * fast_rsqrt((v0 * v0 + v1 * v1) + v2 * v2);
+          f = f > T(0) ? f : T(0);
+          t0 = w0 - P.sigma * (f * v0);
+          t1 = w1 - P.sigma * (f * v1);
+          t2 = w2 - P.sigma * (f * v2);
+        } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
+          t0 = w0 - P.sigma * (v0 - P.t_h * clip1(v0 * P.inv_t_h));
+          t1 = w1 - P.sigma * (v1 - P.t_h * clip1(v1 * P.inv_t_h));
+          t2 = w2 - P.sigma * (v2 - P.t_h * clip1(v2 * P.inv_t_h));
+        }
+        o0.v[m] = P.rho * t0 + P.omr * zv0.v[m];
+        o1.v[m] = P.rho * t1 + P.omr * zv1.v[m];
+        o2.v[m] = P.rho * t2 + P.omr * zv2.v[m];
+        const T e0 = zv0.v[m] - o0.v[m], e1 = zv1.v[m] - o1.v[m], e2 = zv2.v[m] - o2.v[m];
+        sdz += cm ? (e0 * e0 + e1 * e1) + e2 * e2 : T(0);
+        sz += cm ? (zv0.v[m] * zv0.v[m] + zv1.v[m] * zv1.v[m]) + zv2.v[m] * zv2.v[m] : T(0);
+      }
+      if (own) {
+        part[2] += (double)sdz;
+        part[3] += (double)sz;
+        T* d = zn + (int64_t)(q + v.hz) * pl + (int64_t)i1z * v.n2 + c_z;
+        gstore<T, VEC>(d, o0, c_z, v.n2);
+        gstore<T, VEC>(d + zstride, o1, c_z, v.n2);
+        gstore<T, VEC>(d + 2 * zstride, o2, c_z, v.n2);
+      }
+    }
+  }
+  block_sum<4>(part, red);
+  if (hist != nullptr) {
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
+  } else if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
+  }
+}
+
+// ---------------------------------------------------------------- host side
+struct Plan3 {
+  int tiles1, tiles2, seg_len, nseg, ntasks;
+};
+
+static Plan3 plan3(const pcs_pds3d_args* a) {
+  Plan3 p;
+  p.tiles1 = (int)((a->n1 + k3T1 - 1) / k3T1);
+  p.tiles2 = (int)((a->n2 + k3TW - 1) / k3TW);
+  const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
+  // about 8 resident workgroups per CU on 256 CUs; never segments shorter than 8 planes
+  int64_t nseg = (2048 + per_plane - 1) / per_plane;
+  const int64_t max_seg = (a->planes + 7) / 8;
+  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
+  p.seg_len = (int)((a->planes + nseg - 1) / nseg);
+  p.nseg = (int)((a->planes + p.seg_len - 1) / p.seg_len);
+  p.ntasks = (int)(per_plane * p.nseg);
+  return p;
+}
+
+static bool aligned16_3(const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; }
+
+template <typename T, int FK, bool VEC>
+static int launch3(const pcs_pds3d_args* a, hipStream_t st) {
+  const Plan3 p = plan3(a);
+  Vol v;
+  v.n0 = (int)a->n0;
+  v.n1 = (int)a->n1;
+  v.n2 = (int)a->n2;
+  v.plane0 = (int)a->plane0;
+  v.planes = (int)a->planes;
+  v.hx = a->halo_x;
+  v.hz = a->halo_z;
+  v.hg = a->halo_g;
+  v.pitch1 = (uint32_t)(a->n2 * sizeof(T));
+  v.plane_bytes = (uint32_t)(a->n1 * a->n2 * sizeof(T));
+  P3<T> P;
+  P.tau = (T)a->tau;
+  P.sigma = (T)a->sigma;
+  P.inv_sigma = (T)(1.0 / a->sigma);
+  P.rho = (T)a->rho;
+  P.omr = (T)(1.0 - a->rho);
+  const double t_h = (1.0 / a->sigma) * a->lam;  // ProxFuncPostComp: tau*scale with tau = 1/sigma
+  P.t_h = (T)t_h;
+  P.inv_t_h = (T)(1.0 / t_h);
+  const double steps[3] = {a->step0, a->step1, a->step2};
+  for (int k = 0; k < 3; ++k) {
+    P.inv_step[k] = (T)(1.0 / steps[k]);
+    P.unit[k] = steps[k] == 1.0;
+  }
+  P.seg_a = (T)a->seg_a;
+  P.seg_b = (T)a->seg_b;
+  k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, k3NT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn,
+                                                      (const T*)a->g, v, P, a->hkind, a->gkind, a->partials,
+                                                      (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.seg_len,
+                                                      p.ntasks);
+  return launch_status();
+}
+
+template <typename T, bool VEC>
+static int pds3d_v(const pcs_pds3d_args* a, hipStream_t st) {
+  switch (a->fkind) {
+    case PCS_F_NULL: return launch3<T, PCS_F_NULL, VEC>(a, st);
+    case PCS_F_DENOISE: return launch3<T, PCS_F_DENOISE, VEC>(a, st);
+    case PCS_F_GRADBUF: return launch3<T, PCS_F_GRADBUF, VEC>(a, st);
+    default: return PCS_EINVAL;
+  }
+}
+
+template <typename T>
+static int pds3d(const pcs_pds3d_args* a, hipStream_t st) {
+  const bool vec = a->n2 % 4 == 0 && aligned16_3(a->x) && aligned16_3(a->xn) && aligned16_3(a->z) &&
+                   aligned16_3(a->zn) && aligned16_3(a->g);
+  return vec ? pds3d_v<T, true>(a, st) : pds3d_v<T, false>(a, st);
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+extern "C" {
+
+int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a) {
+  if (!a || a->planes < 1 || a->n1 < 1 || a->n2 < 1) return -1;
+  return plan3(a).ntasks;
+}
+
+int64_t pcs_pds3d_ws_bytes(const pcs_pds3d_args* a) {
+  const int64_t nb = pcs_pds3d_nblocks(a);
+  return nb < 0 ? -1 : red_ws_bytes(nb);
+}
+
+int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t st) {
+  if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
+  if (a->n0 < 1 || a->n1 < 1 || a->n2 < 1 || a->planes < 1 || a->plane0 < 0 || a->plane0 + a->planes > a->n0)
+    return PCS_EINVAL;
+  if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return PCS_EINVAL;
+  if (a->gkind < PCS_G_NULL || a->gkind > PCS_G_SEGMENT) return PCS_EINVAL;
+  if (!(a->sigma > 0) || !(a->step0 != 0) || !(a->step1 != 0) || !(a->step2 != 0)) return PCS_EINVAL;
+  if ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_GRADBUF) && !a->g) return PCS_EINVAL;
+  if (a->halo_x < 0 || a->halo_z < 0 || a->halo_g < 0) return PCS_EINVAL;
+  const bool multi = a->planes < a->n0;
+  if (multi && (a->halo_x < 1 || a->halo_z < 1 || (a->fkind != PCS_F_NULL && a->halo_g < 1))) return PCS_EINVAL;
+  const int64_t esz = a->dtype == PCS_F64 ? 8 : 4;
+  if (a->n1 * a->n2 * esz > (1LL << 30) || a->n0 >= (1LL << 30)) return PCS_EUNSUPPORTED;  // one plane <= 1 GiB
+  if (a->hist && (!a->ws || !a->ctrl || !aligned16_3(a->ws) || !aligned16_3(a->partials))) return PCS_EINVAL;
+  if (a->dtype == PCS_F32) return pds3d<float>(a, st);
+  if (a->dtype == PCS_F64) return pds3d<double>(a, st);
+  return PCS_EINVAL;
+}
+
+}  // extern "C"

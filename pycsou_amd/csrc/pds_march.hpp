@@ -185,7 +185,7 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
                                            int gk, int s0, int s1, int c0, T* sm, double (&part)[4]) {
   static_assert(sizeof(T) == 4, "the march kernel is fp32");
   using M = March<H>;
-  constexpr int TS = M::TS, UR = M::UR, TW = M::TW, H4 = M::H4, SH = H4 - H, NT2 = 2 * H + 1;
+  constexpr int TS = M::TS, TW = M::TW, H4 = M::H4, SH = H4 - H, NT2 = 2 * H + 1;
   constexpr int WX = M::WX, WR = M::WR, WG = M::WG, GX = M::GX, GR = M::GR, GG = M::GG;
   constexpr int RR1 = M::RR1, NG2 = M::NG2, NPR2 = M::NPR2, RR3 = M::RR3;
   constexpr int KXN = cdiv(M::NXN, NT), KXP = cdiv(M::NXP, NT), KZ0 = cdiv(M::NZ0, NT), KZ1 = cdiv(M::NZ1, NT);

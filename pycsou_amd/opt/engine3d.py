@@ -1,0 +1,302 @@
+"""Fused PDS engine for 3-D volumes.
+
+Problem family (what a reference script builds for 3-D TV deconvolution / denoising):
+``F = (1/2) * SquaredL2Loss(dim, data=y) [* C]`` with ``C`` a composition of
+``Convolve1D(size, taps, reshape_dims=shape, axis=k)`` (the reference's only 3-D blur,
+``pycsou/linop/conv.py:20-164``), ``K = Gradient(shape, kind='forward')`` in 3-D
+(``pycsou/linop/diff.py:777-882``), ``H = lam * L21Norm(groups=tile(arange(N), 3))`` or
+``lam * L1Norm``, ``G = None / NonNegativeOrthant / Segment``.
+
+One iteration of ``PrimalDualSplitting`` (``pycsou/opt/proxalgs.py:343-394``):
+
+    g = C^T (C x - y)          pcs_conv1d per axis (forward chain), pcs_axpby, the flipped
+                               chain (exactly the reference's Conv^T((2 (Conv x - y)) 0.5))
+    pcs_pds3d_step             x, z, g -> x', z', norm partials, loop control
+
+Volumes are split into slabs of planes (axis 0) across ranks exactly like the 2-D rows of
+``pycsou_amd.parallel.slab``: a slab stores planes ``[plane0 - h, plane0 + planes + h)``; the
+convolution chain runs on the slab's halo'd sub-volume (its axis-0 reach is covered by the
+x halo of ``2 reach + 1`` planes), the update needs one plane of z halo.  Per iteration the
+ranks all-gather the four norm sums and exchange the x' / z' halo planes.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _lib as L
+from .. import _ops as O
+from ..core.functional import ProxFuncPostComp
+from ..core.linop import LinOpComp
+from ..core.map import DiffMapComp
+from ..func.base import IndicatorFunctional, NullDifferentiableFunctional, NullProximableFunctional
+from ..func.penalty import L1Norm, L21Norm
+from ..linop.conv import Convolve1DOp
+from ..linop.diff import GradientOp
+from ..parallel.slab import SlabLayout
+from .engine import _half_loss_data
+
+
+def conv_chain(C, shape):
+    """The Convolve1D operators of a composition in application order, or None."""
+    if isinstance(C, Convolve1DOp):
+        return [C] if tuple(C.dims) == tuple(shape) else None
+    if isinstance(C, LinOpComp):
+        first, then = conv_chain(C.LinOp2, shape), conv_chain(C.LinOp1, shape)
+        return None if first is None or then is None else first + then
+    return None
+
+
+def match_pds3d(F, G, H, K, has_H):
+    """Engine spec dict if (F, G, H, K) is a fused 3-D problem, else None."""
+    if not has_H or not isinstance(K, GradientOp) or len(K.dims) != 3 or K.kind != 'forward':
+        return None
+    shape = tuple(K.dims)
+    N = int(np.prod(shape))
+    spec = {'ndim': 3, 'shape': shape, 'steps': tuple(K.steps)}
+    base, lam = H, 1.0
+    if isinstance(H, ProxFuncPostComp):
+        if H.shift != 0:
+            return None
+        base, lam = H.prox_func, float(H.scale)
+    if isinstance(base, L21Norm) and base.pixel_d == 3 and base.dim == 3 * N:
+        spec['hkind'] = L.PCS_H_L21
+    elif isinstance(base, L1Norm) and base.dim == 3 * N:
+        spec['hkind'] = L.PCS_H_L1
+    else:
+        return None
+    spec['lam'] = lam
+    if G is None or isinstance(G, NullProximableFunctional):
+        spec['gkind'], spec['seg'] = L.PCS_G_NULL, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'nonneg':
+        spec['gkind'], spec['seg'] = L.PCS_G_NONNEG, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'segment':
+        spec['gkind'], spec['seg'] = L.PCS_G_SEGMENT, G.params
+    else:
+        return None
+    if F is None or isinstance(F, NullDifferentiableFunctional):
+        spec['fkind'] = L.PCS_F_NULL
+        return spec
+    s = _half_loss_data(F)
+    if s is not None and O.numel(s) == N:
+        spec['fkind'], spec['shift'] = L.PCS_F_DENOISE, s
+        return spec
+    if isinstance(F, DiffMapComp):
+        chain = conv_chain(F.map2, shape)
+        s = _half_loss_data(F.map1)
+        if chain and s is not None and O.numel(s) == N:
+            spec['fkind'], spec['shift'], spec['chain'] = L.PCS_F_GRADBUF, s, chain
+            return spec
+    return None
+
+
+class PDS3DEngine:
+    """Device state + loop of one rank's slab (the whole volume when world == 1)."""
+
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, comm=None, rank=0, world=1, chunk=8, use_graph=True):
+        self.lib = L.gpu()
+        self.spec, self.dtype, self.comm = spec, dtype, comm
+        self.rank, self.world = int(rank), int(world)
+        n0, n1, n2 = spec['shape']
+        self.n0, self.n1, self.n2 = n0, n1, n2
+        plane = n1 * n2
+        self.plane = plane
+        self.lay = lay = SlabLayout(n0, plane, rank, world)  # rows of the layout = planes
+        self.row0, self.rows = lay.row0, lay.rows
+        fk = spec['fkind']
+        self.fkind = fk
+        dev = torch.device('cuda', torch.cuda.current_device())
+        self.chain = []
+        reach = 0
+        if fk == L.PCS_F_GRADBUF:
+            for op in spec['chain']:
+                k, off = op.k, op.off
+                self.chain.append((op.axis, op._h.get(dtype), op._hf.get(dtype), k, off))
+                if op.axis == 0:
+                    reach += max(off, k - 1 - off)
+        hx = 2 * reach + 1 if fk == L.PCS_F_GRADBUF else 1
+        hz = 1
+        hg = hx if fk == L.PCS_F_GRADBUF else 1
+        if world > 1 and self.rows < max(hx, hz):
+            raise ValueError(f'slab of {self.rows} planes is thinner than its halo ({hx} planes)')
+        self.hx, self.hz, self.hg = hx, hz, hg
+        N = n0 * plane
+        x0d, z0d = O.to_dev(x0, dtype), O.to_dev(z0, dtype)
+        self.X = [lay.window(x0d, hx) for _ in range(2)]
+        self.Z = [torch.cat([lay.window(z0d[c * N:(c + 1) * N], hz) for c in range(3)]) for _ in range(2)]
+        self.gbuf = None
+        if fk in (L.PCS_F_DENOISE, L.PCS_F_GRADBUF):
+            self.yw = lay.window(-O.to_dev(spec['shift'], dtype), hg)  # y = -shift exactly
+        if fk == L.PCS_F_GRADBUF:
+            nloc = (self.rows + 2 * hx) * plane
+            self.T = [torch.empty(nloc, dtype=dtype, device=dev) for _ in range(2)]
+            self.sub_dims = (self.rows + 2 * hx, n1, n2)
+            # planes of the sub-volume outside the image: the residual is 0 there
+            self.zero_planes = [j for j in range(self.rows + 2 * hx)
+                                if not 0 <= self.row0 - hx + j < n0]
+            # the chain's final buffer is fixed by its length: forward + adjoint passes
+            self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
+        a = L.Pds3Args()
+        a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+        a.fkind, a.hkind, a.gkind = fk, spec['hkind'], spec['gkind']
+        a.n0, a.n1, a.n2, a.plane0, a.planes = n0, n1, n2, self.row0, self.rows
+        a.halo_x, a.halo_z, a.halo_g = hx, hz, hg
+        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+        a.step0, a.step1, a.step2 = spec['steps']
+        a.seg_a, a.seg_b = spec['seg']
+        if fk == L.PCS_F_DENOISE:
+            a.g = self.yw.data_ptr()
+        elif fk == L.PCS_F_GRADBUF:
+            a.g = self.gbuf.data_ptr()
+        self.nblocks = int(self.lib.pcs_pds3d_nblocks(ctypes.byref(a)))
+        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+        a.partials = self.partials.data_ptr()
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
+        a.ctrl = self.ctrl.data_ptr()
+        self.ws = torch.zeros(int(self.lib.pcs_pds3d_ws_bytes(ctypes.byref(a))) // 8 + 2, dtype=torch.float64,
+                              device=dev)
+        a.ws = self.ws.data_ptr()
+        self.base_args = a
+        self.args = [self._args_for(p) for p in (0, 1)]
+        self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
+        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c) for c in range(3)])
+                      for q in (0, 1)] if world > 1 else [{}, {}]
+        self.hist = None
+        self.graph = None
+        self.chunk = max(2, chunk + chunk % 2)
+        self.use_graph = use_graph and world == 1
+
+    def _args_for(self, p):
+        b = L.Pds3Args()
+        ctypes.pointer(b)[0] = self.base_args
+        b.x, b.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+        b.z, b.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        return b
+
+    # ---- grad F = C^T (C x - y) on the slab's sub-volume
+    def _conv_into(self, src, dst, axis, taps, k, off, st):
+        L.check(self.lib.pcs_conv1d(self.base_args.dtype, L.ptr(src), L.ptr(dst), 3, L.i64s(self.sub_dims),
+                                    int(axis), L.ptr(taps), int(k), int(off), st), 'pcs_conv1d')
+
+    def _gradient(self, p, st):
+        cur, j = self.X[p], 0
+        for axis, h, _, k, off in self.chain:
+            dst = self.T[j % 2]
+            self._conv_into(cur, dst, axis, h, k, off, st)
+            cur, j = dst, j + 1
+        # r = (C x) + (-y): the reference's residual, exact
+        L.check(self.lib.pcs_axpby(self.base_args.dtype, L.ptr(cur), L.ptr(self.yw), L.ptr(cur), cur.numel(), 1.0,
+                                   -1.0, st), 'pcs_axpby')
+        if self.zero_planes:
+            v = cur.view(-1, self.plane)
+            for jz in self.zero_planes:
+                v[jz].zero_()
+        for axis, _, hf, k, off in reversed(self.chain):
+            dst = self.T[j % 2]
+            self._conv_into(cur, dst, axis, hf, k, k - 1 - off, st)
+            cur, j = dst, j + 1
+        assert cur is self.gbuf
+
+    def _step(self, p, hist):
+        st = L.stream()
+        if self.fkind == L.PCS_F_GRADBUF:
+            self._gradient(p, st)
+        a = self.args[p]
+        a.hist = None if hist is None else hist.data_ptr()
+        L.check(self.lib.pcs_pds3d_step(ctypes.byref(a), st), 'pcs_pds3d_step')
+
+    # phases of a multi-rank iteration (pycsou_amd.parallel.run_local interleaves them)
+    def _compute(self, p):
+        self._step(p, None)
+        L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), self.nblocks, L.ptr(self.sums), L.stream()),
+                'pcs_reduce_partials')
+
+    def _finalize(self):
+        L.check(self.lib.pcs_pds_reduce_finalize(L.ptr(self.gathered), self.world, L.ptr(self.ctrl),
+                                                 L.ptr(self.hist), L.stream()), 'pcs_pds_reduce_finalize')
+
+    def iteration(self, p):
+        if self.world == 1:
+            self._step(p, self.hist)
+            return
+        self._compute(p)
+        self.comm.allgather(self.sums, self.gathered)
+        self._finalize()
+        self.comm.exchange(self.halos[1 - p])
+
+    # ---- loops
+    def init_loop(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        total = max(min_iter, max_iter) + 1
+        hist_len = 2 * total + 2
+        if self.hist is None or self.hist.numel() < hist_len:
+            self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
+            self.graph = None
+        self.hist.fill_(float('nan'))
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
+                                        int(has_dual), int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
+        self._p = 0
+        return total
+
+    def _chunk(self):
+        for i in range(self.chunk):
+            self.iteration(i % 2)
+
+    def advance(self, k):
+        """Enqueue k iterations (k a multiple of the chunk when graphs are used)."""
+        if self.use_graph:
+            if self.graph is None:
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._chunk()
+                self.graph = g
+            for _ in range(k // self.chunk):
+                self.graph.replay()
+            return
+        for _ in range(k):
+            self.iteration(self._p)
+            self._p ^= 1
+
+    def iterations(self):
+        return int(self.ctrl.view(torch.int32)[0].item())
+
+    def stopped(self):
+        return int(self.ctrl.view(torch.int32)[1].item()) != 0
+
+    def result(self):
+        """(n_iter, own planes of x, own planes of z (3 components), hist [n, 2])."""
+        torch.cuda.synchronize()
+        n = self.iterations()
+        q = n % 2
+        x = self.lay.rows_view(self.X[q], self.hx, 0, self.rows).clone()
+        z = torch.cat([self.lay.rows_view(self.Z[q], self.hz, 0, self.rows, c) for c in range(3)])
+        h = self.hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
+        return n, x, z, h
+
+    def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        total = self.init_loop(max_iter, min_iter, accuracy_threshold, has_dual)
+        step = self.chunk
+        done = 0
+        while done < total:
+            self.advance(step)
+            done += step
+            if self.stopped():
+                break
+        return self.result()
+
+    def time_step_kernel(self, n):
+        """Mean duration (ms) of pcs_pds3d_step alone over n eager launches (HIP events)."""
+        st = torch.cuda.current_stream()
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, 2 * n + 6, L.stream()),
+                'pcs_ctrl_init2')
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for i in range(n):
+            a = self.args[i % 2]
+            a.hist = None
+            evs[i][0].record(st)
+            L.check(self.lib.pcs_pds3d_step(ctypes.byref(a), L.stream()), 'pcs_pds3d_step')
+            evs[i][1].record(st)
+        torch.cuda.synchronize()
+        return float(np.mean([s.elapsed_time(e) for s, e in evs]))

@@ -190,8 +190,9 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         if self.engine_mode in (False, 'generic'):
             return None
         from .engine import match_pds2d
-        return match_pds2d(None if isinstance(self.F, NullDifferentiableFunctional) else self.F, self.G, self.H,
-                           self.K, self._H)
+        from .engine3d import match_pds3d
+        F = None if isinstance(self.F, NullDifferentiableFunctional) else self.F
+        return match_pds2d(F, self.G, self.H, self.K, self._H) or match_pds3d(F, self.G, self.H, self.K, self._H)
 
     def iterate(self):
         spec = self._fused_spec()
@@ -200,10 +201,12 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
                 raise ValueError('problem does not match the fused PDS engine')
             return self._iterate_generic()
         from .engine import PDS2DEngine
+        from .engine3d import PDS3DEngine
         dtype = self._compute_dtype()
         x0 = O.to_dev(self.x0, dtype)
         z0 = O.to_dev(self.z0, dtype)
-        self._engine = PDS2DEngine(spec, dtype, self.tau, self.sigma, self.rho, x0, z0)
+        eng = PDS3DEngine if spec.get('ndim', 2) == 3 else PDS2DEngine
+        self._engine = eng(spec, dtype, self.tau, self.sigma, self.rho, x0, z0)
         n, x, z, hist = self._engine.run(self.max_iter, self.min_iter, self.accuracy_threshold, has_dual=True)
         self.iter = n
         rows = [[i, hist[i, 0], hist[i, 1]] for i in range(n)]

@@ -212,3 +212,55 @@ def test_pds_fused_crop_vs_oracle_fp32_512():
     assert pds._engine is not None and pds.iter == 20
     assert rel(est['primal_variable'], xr) < 5e-5
     assert rel(est['dual_variable'], zr) < 5e-5
+
+
+FUSED_3D = [n for n in pds_case_names() if '3d' in n]
+
+
+@pytest.mark.parametrize('name', FUSED_3D)
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+def test_pds3d_fused_matches_reference(name, dtype):
+    """3-D volumes: Convolve1D chain + 3-D Gradient + L21/L1 through PDS3DEngine."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    c = pds_case(name)
+    pds = build(c, dtype, engine='fused')
+    _check(pds, c, dtype)
+    assert isinstance(pds._engine, PDS3DEngine)
+
+
+def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10):
+    """A 3-D TV deconvolution case (separable 15-tap Gaussian along every axis), built like
+    the golden cases so tests/cases.oracle_pds can run it."""
+    rng = np.random.default_rng(seed)
+    shape = (n, n, n)
+    xs = np.zeros(shape)
+    for _ in range(12):
+        lo = rng.integers(0, n, 3)
+        hi = np.minimum(n, lo + rng.integers(n // 8, n // 2, 3))
+        xs[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = rng.uniform(0, 1)
+    r = np.arange(15) - 7
+    taps = np.exp(-0.5 * (r / 2.0) ** 2)
+    taps /= taps.sum()
+    from oracle import pylops1 as P
+    N = n ** 3
+    v = xs.ravel()
+    for a in range(3):
+        v = P.Convolve1D(N, taps, offset=7, dims=shape, dir=a).matvec(v)
+    y = v + 0.01 * rng.standard_normal(N)
+    c = {'shape': shape, 'taps': taps, 'y': y,
+         'meta': {'kind': 'forward', 'hname': 'l21', 'lam': lam, 'niter': niter}}
+    return c
+
+
+def test_pds3d_128_fp64_vs_oracle():
+    """C5 parity size: 128^3 fp64, 10 iterations vs the CPU oracle."""
+    c = _vol_problem(128, np.float64)
+    pds = build(c, np.float64, engine='fused')
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    est, _, diag = pds.iterate()
+    assert pds.iter == 10
+    x_ref, z_ref, d_ref = oracle_pds(c)
+    assert rel(est['primal_variable'], x_ref) < 1e-10
+    assert rel(est['dual_variable'], z_ref) < 1e-10
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:],
+                               np.asarray(d_ref['primal'])[1:], rtol=1e-8)
