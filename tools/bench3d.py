@@ -1,0 +1,98 @@
+"""3-D TV-deconvolution throughput on one GPU.
+
+C4: 512^3 fp32, C5: 1024^3 fp64 -- a piecewise-constant phantom blurred by a 15-tap Gaussian
+(sigma 2) along each axis (three Convolve1D, the reference's 3-D blur), y = h*x + 0.01 N(0,1),
+PDS with K = Gradient(kind='forward') in 3-D and H = 0.05 * L21Norm (3 components), built
+through the public API and run by PDS3DEngine (hipGraph chunks).  Prints one JSON line:
+it/s, ms per iteration, the update kernel's mean duration and the algorithmic rates.
+
+  python tools/bench3d.py --size 512 --dtype f32 --steps 20 --warmup 4
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def build(n, dtype, seed=0):
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.conv import Convolve1D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    shape = (n, n, n)
+    N = n ** 3
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    xs = torch.zeros(shape, dtype=dtype, device='cuda')
+    rng = np.random.default_rng(seed)
+    for _ in range(32):
+        lo = rng.integers(0, n, 3)
+        hi = np.minimum(n, lo + rng.integers(n // 16, n // 3, 3))
+        xs[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = float(rng.uniform(0, 1))
+    r = np.arange(15) - 7
+    taps = np.exp(-0.5 * (r / 2.0) ** 2)
+    taps /= taps.sum()
+    C = None
+    for ax in range(3):
+        Ci = Convolve1D(N, taps, reshape_dims=shape, axis=ax)
+        Ci.lipschitz_cst = Ci.diff_lipschitz_cst = 1.0
+        C = Ci if C is None else Ci * C
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
+    del xs
+    K = Gradient(shape=shape, kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(sum(4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2
+                                                               for _ in range(3))))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
+    H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+               z0=torch.zeros(3 * N, dtype=dtype, device='cuda'), verbose=None)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--size', type=int, default=512)
+    ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=4)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    dtype = torch.float32 if args.dtype == 'f32' else torch.float64
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    t0 = time.time()
+    pds = build(args.size, dtype)
+    spec = pds._fused_spec()
+    assert spec is not None and spec['ndim'] == 3
+    chunk = 2
+    eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, chunk=chunk)
+    del pds
+    K = args.steps + args.steps % 2
+    W = args.warmup + args.warmup % 2
+    eng.init_loop(W + K + 4, W + K + 4, -1.0)
+    eng.advance(W)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    eng.advance(K)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / K
+    assert eng.iterations() == W + K
+    kms = eng.time_step_kernel(min(K, 10))
+    N = args.size ** 3
+    elem = 4 if dtype == torch.float32 else 8
+    alg = 9 * N * elem  # (2d+3) N words, d = 3
+    print(json.dumps({'workload': f'3-D TV-deconv {args.size}^3 {args.dtype}, 15-tap Gaussian per axis, '
+                                  f'0.05*L21, PDS3DEngine', 'it_per_s': round(1e3 / ms, 3), 'ms_per_iter': round(ms, 4),
+                      'update_kernel_ms': round(kms, 4), 'alg_bytes_per_iter': alg,
+                      'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
+                      'update_kernel_GBps': round(alg / (kms * 1e-3) / 1e9, 1), 'setup_s': round(time.time() - t0, 1)}))
+
+
+if __name__ == '__main__':
+    main()
