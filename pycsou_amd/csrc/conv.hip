@@ -127,15 +127,178 @@ static int conv2d(const void* x, void* out, int64_t n0, int64_t n1, const void* 
   return launch_status();
 }
 
+// ---- fast paths for taps k <= 15 (zero-padded to 15: out[j] = sum_{t<15} h'[t] x[j + off - t])
+constexpr int kC1K = 15;
+
+template <typename T>
+struct V16 {  // 16 bytes of T
+  static constexpr int N = 16 / sizeof(T);
+  T v[N];
+};
+template <typename T>
+__device__ __forceinline__ V16<T> ldv(const T* p) {
+  V16<T> r;
+  *reinterpret_cast<uint4*>(r.v) = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void stv(T* p, const V16<T>& r) {
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(r.v);
+}
+
+// Strided axis (stride sa >= 16 B, 16-B aligned rows): a thread owns 16 B of consecutive inner
+// elements and RUN consecutive outputs along the axis; every input row it streams feeds up to
+// 15 outputs held in registers (coalesced 16-B loads, each input read once per run).
+template <typename T, int RUN>
+__global__ __launch_bounds__(256) void k_conv1d_strided(const T* __restrict__ x, T* __restrict__ out, int64_t outer,
+                                                         int64_t na, int64_t sa, const T* __restrict__ taps, int k,
+                                                         int off) {
+  constexpr int VN = V16<T>::N;
+  T h[kC1K];
+#pragma unroll
+  for (int t = 0; t < kC1K; ++t) h[t] = t < k ? taps[t] : T(0);
+  const int64_t ng = sa / VN, nrun = (na + RUN - 1) / RUN;
+  const int64_t total = outer * nrun * ng;
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cg = id % ng, rest = id / ng, jr = rest % nrun, o = rest / nrun;
+    const int64_t j0 = jr * RUN;
+    const T* xb = x + o * na * sa + cg * VN;
+    T acc[RUN][VN];
+#pragma unroll
+    for (int m = 0; m < RUN; ++m)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) acc[m][e] = T(0);
+    // input row u = j0 + off - (15-1) + q feeds output m with tap t = m + 14 - q
+#pragma unroll
+    for (int q = 0; q < RUN + kC1K - 1; ++q) {
+      const int64_t u = j0 + off - (kC1K - 1) + q;
+      V16<T> v;
+      if (u >= 0 && u < na) {
+        v = ldv(xb + u * sa);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) v.v[e] = T(0);
+      }
+#pragma unroll
+      for (int m = 0; m < RUN; ++m) {
+        const int t = m + kC1K - 1 - q;
+        if (t >= 0 && t < kC1K) {
+#pragma unroll
+          for (int e = 0; e < VN; ++e) acc[m][e] += h[t] * v.v[e];
+        }
+      }
+    }
+    T* ob = out + o * na * sa + cg * VN;
+#pragma unroll
+    for (int m = 0; m < RUN; ++m) {
+      if (j0 + m < na) {
+        V16<T> r;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) r.v[e] = acc[m][e];
+        stv(ob + (j0 + m) * sa, r);
+      }
+    }
+  }
+}
+
+// Contiguous axis (stride 1): a block owns a 16*256-byte segment of one row (staged in LDS
+// with a 16-B aligned halo of >= 14 elements each side); thread i computes the 16 B of
+// outputs at 16*i from 16-B LDS reads.  SH = (off + 2*VN - 14) mod VN ... selects the window
+// alignment at compile time.
+template <typename T, int SHIFT>
+__global__ __launch_bounds__(256) void k_conv1d_contig(const T* __restrict__ x, T* __restrict__ out, int64_t rows,
+                                                        int64_t na, const T* __restrict__ taps, int k, int off) {
+  constexpr int VN = V16<T>::N;
+  constexpr int SEG = 256 * VN;         // outputs per block
+  constexpr int HALO = 16;              // elements (multiple of VN, >= 14)
+  constexpr int NW = (VN + kC1K - 1 + SHIFT + VN - 1) / VN;  // 16-B reads per window
+  __shared__ __attribute__((aligned(16))) T sm[SEG + 2 * HALO + 2 * VN];
+  T h[kC1K];
+#pragma unroll
+  for (int t = 0; t < kC1K; ++t) h[t] = t < k ? taps[t] : T(0);
+  const int64_t nseg = (na + SEG - 1) / SEG;
+  const int64_t r = blockIdx.x / nseg, sgi = blockIdx.x - r * nseg;
+  if (r >= rows) return;
+  const int64_t c0 = sgi * SEG;
+  const T* xr = x + r * na;
+  // stage [c0 - HALO, c0 + SEG + HALO) (zero outside the row), 16 B per thread-load
+  for (int e = threadIdx.x; e < (SEG + 2 * HALO) / VN; e += 256) {
+    const int64_t c = c0 - HALO + (int64_t)e * VN;
+    V16<T> v;
+    if (c >= 0 && c + VN <= na) {
+      v = ldv(xr + c);
+    } else {
+#pragma unroll
+      for (int q = 0; q < VN; ++q) v.v[q] = (c + q >= 0 && c + q < na) ? xr[c + q] : T(0);
+    }
+    stv(sm + e * VN, v);
+  }
+  __syncthreads();
+  // outputs j = c0 + VN*i + m read inputs j + off - t, t < 15: LDS index
+  // VN*i + m + HALO + off - 14 + (14 - t); window start (aligned) base = VN*i + ((HALO + off - 14) & ~(VN-1))
+  const int i = threadIdx.x;
+  const int start = HALO + off - (kC1K - 1);  // >= 2 since off >= 0
+  const int abase = VN * i + (start & ~(VN - 1));
+  T w[NW * VN];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const V16<T> v = *reinterpret_cast<const V16<T>*>(sm + abase + q * VN);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) w[q * VN + e] = v.v[e];
+  }
+  V16<T> o;
+#pragma unroll
+  for (int m = 0; m < VN; ++m) {
+    T acc = T(0);
+#pragma unroll
+    for (int t = 0; t < kC1K; ++t) acc += h[t] * w[SHIFT + m + (kC1K - 1 - t)];
+    o.v[m] = acc;
+  }
+  const int64_t j = c0 + VN * i;
+  if (j + VN <= na) {
+    stv(out + r * na + j, o);
+  } else {
+#pragma unroll
+    for (int m = 0; m < VN; ++m)
+      if (j + m < na) out[r * na + j + m] = o.v[m];
+  }
+}
+
 template <typename T>
 static int conv1d(const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps, int k, int off,
                   hipStream_t st) {
   if (!x || !out || !taps || !dims || ndim < 1 || ndim > 3 || axis < 0 || axis >= ndim || k < 1 || off < 0 ||
       off >= k)
     return PCS_EINVAL;
-  int64_t N = 1, sa = 1;
+  int64_t N = 1, sa = 1, outer = 1;
   for (int i = 0; i < ndim; ++i) N *= dims[i];
   for (int i = axis + 1; i < ndim; ++i) sa *= dims[i];
+  for (int i = 0; i < axis; ++i) outer *= dims[i];
+  constexpr int VN = V16<T>::N;
+  const bool al = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (k <= kC1K && al && sa > 1 && sa % VN == 0) {
+    constexpr int RUN = sizeof(T) == 4 ? 16 : 8;
+    const int64_t work = outer * ((dims[axis] + RUN - 1) / RUN) * (sa / VN);
+    k_conv1d_strided<T, RUN><<<grid_for(work, 256, 1u << 20), 256, 0, st>>>(
+        (const T*)x, (T*)out, outer, dims[axis], sa, (const T*)taps, k, off);
+    return launch_status();
+  }
+  if (k <= kC1K && al && sa == 1 && dims[axis] % VN == 0) {
+    const int64_t rows = outer, na = dims[axis];
+    const int64_t nseg = (na + 256 * VN - 1) / (256 * VN);
+    if (rows * nseg < (1LL << 31)) {
+      const int s = (16 + off - (kC1K - 1)) & (VN - 1);
+      const unsigned g = (unsigned)(rows * nseg);
+      switch (s) {
+        case 0: k_conv1d_contig<T, 0><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
+        case 1: k_conv1d_contig<T, 1><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
+        case 2: k_conv1d_contig<T, 2><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
+        default: k_conv1d_contig<T, 3><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
+      }
+      return launch_status();
+    }
+  }
   k_conv1d<T><<<grid_for(N, 256), 256, 0, st>>>((const T*)x, (T*)out, N, dims[axis], sa, (const T*)taps, k, off);
   return launch_status();
 }

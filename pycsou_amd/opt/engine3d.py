@@ -189,10 +189,14 @@ class PDS3DEngine:
         # r = (C x) + (-y): the reference's residual, exact
         L.check(self.lib.pcs_axpby(self.base_args.dtype, L.ptr(cur), L.ptr(self.yw), L.ptr(cur), cur.numel(), 1.0,
                                    -1.0, st), 'pcs_axpby')
-        if self.zero_planes:
+        if self.zero_planes:  # at most one run at each end of the sub-volume
             v = cur.view(-1, self.plane)
-            for jz in self.zero_planes:
-                v[jz].zero_()
+            lo = [j for j in self.zero_planes if j < self.hx]
+            hi = [j for j in self.zero_planes if j >= self.hx]
+            if lo:
+                v[lo[0]:lo[-1] + 1].zero_()
+            if hi:
+                v[hi[0]:hi[-1] + 1].zero_()
         for axis, _, hf, k, off in reversed(self.chain):
             dst = self.T[j % 2]
             self._conv_into(cur, dst, axis, hf, k, k - 1 - off, st)
