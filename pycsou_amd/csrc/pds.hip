@@ -141,14 +141,13 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   return launch_status();
 }
 
-// ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel on the column-interior
-// strips, the tile kernel on the boundary strips, then the reduction (+ loop control)
+// ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel (pds_march.hpp) on every
+// 64-column strip, reduction + loop control in its last workgroups
 constexpr int kMarchNT = 256;
 
 struct MarchPlan {
-  int tiles_x, bl, br;           // 64-column strips; boundary strips on the left / right
-  int mstrips, seg_len, ntasks;  // march kernel: interior strips, rows per task, tasks
-  int btiles;                    // tile kernel: tiles on the boundary strips
+  int tiles_x;                   // 64-column strips
+  int seg_len, ntasks;           // rows per task, tasks (strips x row segments)
 };
 
 // resident workgroups of the march kernel on the whole device (queried once)
@@ -160,8 +159,8 @@ static int march_slots() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_march<float, H, kMarchNT>, kMarchNT, 0) !=
-            hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_march<float, H, PCS_H_L21, kMarchNT>, kMarchNT,
+                                                     0) != hipSuccess ||
         nb < 1)
       nb = 3;
     (void)hipGetLastError();
@@ -170,25 +169,21 @@ static int march_slots() {
   return slots;
 }
 
-// One march task = one interior 64-column strip x one row segment; as many segments as fill
-// the device in one wave of resident workgroups (equal segments: no tail).  False when no
-// strip is column-interior (narrow images) -> tile kernel only.
+// One march task = one 64-column strip x one row segment; as many segments as fill the
+// device in one wave of resident workgroups.  False for narrow images (the tile kernel).
 template <int H>
 static bool march_plan(const pcs_pds2d_args* a, MarchPlan* p) {
   using M = March<H>;
   constexpr int TS = M::TS;
   p->tiles_x = (int)((a->n1 + M::TW - 1) / M::TW);
-  if (p->tiles_x < 2) return false;  // narrow images: the tile kernel
-  p->bl = p->br = 0;                 // every strip marches (edge columns clamp + zero)
-  p->mstrips = p->tiles_x;
+  if (p->tiles_x < 2) return false;
   const int64_t steps = (a->rows + TS - 1) / TS;
-  int64_t nseg = march_slots<H>() / p->mstrips;
+  int64_t nseg = march_slots<H>() / p->tiles_x;
   nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
   const int64_t steps_per = (steps + nseg - 1) / nseg;
   p->seg_len = (int)(steps_per * TS);
   nseg = (a->rows + p->seg_len - 1) / p->seg_len;
-  p->ntasks = (int)(p->mstrips * nseg);
-  p->btiles = 0;
+  p->ntasks = (int)(p->tiles_x * nseg);
   return true;
 }
 
@@ -198,6 +193,7 @@ static bool use_march(const pcs_pds2d_args* a) {
   if (disabled) return false;
   const int t = tier_for(a->half);
   if (a->dtype != PCS_F32 || a->fkind != PCS_F_SEPCONV || (t != 3 && t != 7) || !make_slab(a).vec) return false;
+  if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return false;
   const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
                                              : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
   // 32-bit indexing and buffer views of at most 2^30 bytes (pds_march.hpp kOOB)
@@ -206,30 +202,23 @@ static bool use_march(const pcs_pds2d_args* a) {
   return t == 3 ? march_plan<3>(a, &p) : march_plan<7>(a, &p);
 }
 
-template <int H>
+template <int H, int HK>
 static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
   MarchPlan p;
   if (!march_plan<H>(a, &p)) return PCS_EINVAL;
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
-  k_pds2d_march<float, H, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
+  k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
-      (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials,
-      (Ctrl*)a->ctrl, p.btiles > 0 ? nullptr : a->hist, a->ws, p.bl, p.mstrips, p.seg_len, p.ntasks);
-  if (p.btiles > 0) {
-    constexpr int TH = Tile<float>::TH, NT = Tile<float>::NT;
-    const int nb = p.bl + p.br;
-    k_pds2d<float, PCS_F_SEPCONV, H, TH, NT><<<(unsigned)p.btiles, NT, 0, st>>>(
-        (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y, nullptr,
-        (const float*)a->taps0, (const float*)a->taps1, a->half, s64, P, a->hkind, a->gkind,
-        a->partials + 4 * (int64_t)p.ntasks, (Ctrl*)a->ctrl, nullptr, nullptr, nb, p.btiles, p.bl,
-        p.tiles_x - nb);
-  }
-  if (a->hist != nullptr && p.btiles > 0)
-    k_reduce_finalize<<<1, kRedThreads, 0, st>>>(a->partials, (int64_t)p.ntasks + p.btiles, (Ctrl*)a->ctrl,
-                                                  a->hist);
+      (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
+      a->ws, p.tiles_x, p.seg_len, p.ntasks);
   return launch_status();
+}
+
+template <int H>
+static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
+  return a->hkind == PCS_H_L21 ? launch_march<H, PCS_H_L21>(a, st) : launch_march<H, PCS_H_L1>(a, st);
 }
 
 template <typename T>
@@ -271,7 +260,7 @@ int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
     MarchPlan p;
     if (tier_for(a->half) == 3) march_plan<3>(a, &p);
     else march_plan<7>(a, &p);
-    return (int64_t)p.ntasks + p.btiles;
+    return (int64_t)p.ntasks;
   }
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);

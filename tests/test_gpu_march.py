@@ -1,0 +1,113 @@
+"""The row-marching fused step (pds_march.hpp: fp32, separable PSF of half-width <= 7, n1 >= 128,
+n1 % 4 == 0) against the fp64 oracle, on shapes that exercise its edges: partial last strip,
+several row segments with a short last one, both tap tiers (3, 7) and PSFs narrower than their
+tier, L1 / L21, every prox_G kind, non-unit gradient steps.
+
+Tolerance: relative L2 of x and z <= 5e-5 after 12 iterations (fp32 against fp64, as the golden
+fp32 cases), diagnostics to 2e-2 relative, iteration counts exact.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import pycsou_ref as OR
+from tests.cases import rel
+
+pytestmark = pytest.mark.gpu
+
+NITER = 12
+
+
+def _problem(shape, psf_len, hname, gname, steps, seed):
+    rng = np.random.default_rng(seed)
+    n0, n1 = shape
+    N = n0 * n1
+    xs = OR.phantom(shape, seed=seed)
+    r = np.arange(psf_len) - psf_len // 2
+    t0 = np.exp(-0.5 * (r / 1.7) ** 2)
+    t1 = np.exp(-0.5 * (r / 2.3) ** 2)
+    psf = np.outer(t0 / t0.sum(), t1 / t1.sum())
+    return dict(shape=shape, N=N, psf=psf, y=xs.ravel() + 0.05 * rng.standard_normal(N), hname=hname, gname=gname,
+                steps=steps, lam=0.05)
+
+
+def _oracle(p):
+    from oracle import pylops1 as P
+    shape, N, psf, y = p['shape'], p['N'], p['psf'], p['y']
+    off = tuple(P.pycsou_offset(n) for n in psf.shape)
+    C = P.Convolve2D(N, psf, shape, offset=off)
+    K = P.Gradient(shape, sampling=p['steps'], edge=True, kind='forward')
+    if p['hname'] == 'l21':
+        hprox = OR.postcomp(lambda v, t: OR.prox_l21_pixel(v, t, 2), p['lam'])
+    else:
+        hprox = OR.postcomp(OR.prox_l1, p['lam'])
+    gprox = {'nonneg': lambda v, t: OR.proj_nonnegative_orthant(v),
+             'segment': lambda v, t: OR.proj_segment(v, 0.0, 1.0)}.get(p['gname'], lambda v, t: v)
+    beta = 1.0
+    lip = np.sqrt(sum(4.0 / s ** 2 for s in p['steps']))
+    tau, sigma = OR.pds_step_sizes(beta, lip)[:2]
+    x, z, d = OR.pds(lambda v: C.rmatvec((2 * (C.matvec(v) + (-y))) * 0.5), gprox, K.matvec, K.rmatvec,
+                     lambda w, s: OR.fenchel_prox(hprox, w, s), tau, sigma, 0.9, np.zeros(N), np.zeros(2 * N),
+                     max_iter=NITER - 1, min_iter=NITER - 1, accuracy_threshold=0.0)
+    return x, z, d, lip
+
+
+def _fused(p, lip):
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L1Norm, L21Norm, NonNegativeOrthant, Segment
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    shape, N = p['shape'], p['N']
+    C = Convolve2D(N, p['psf'], shape)
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    K = Gradient(shape, step=p['steps'], kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = lip
+    H = p['lam'] * (L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)) if p['hname'] == 'l21' else L1Norm(dim=2 * N))
+    G = {'nonneg': NonNegativeOrthant(N), 'segment': Segment(N, 0.0, 1.0)}.get(p['gname'], None)
+    pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=p['y'].astype(np.float32)) * C, G=G, H=H, K=K,
+              x0=np.zeros(N, np.float32), z0=np.zeros(2 * N, np.float32), max_iter=NITER - 1, min_iter=NITER - 1,
+              accuracy_threshold=0.0, verbose=None, engine='fused')
+    est, _, diag = pds.iterate()
+    assert pds._engine is not None and pds.iter == NITER
+    return est['primal_variable'], est['dual_variable'], diag
+
+
+CASES = [
+    # shape, psf length, H, G, steps
+    ((300, 200), 15, 'l21', '', (1.0, 1.0)),       # tier 7, partial last strip (200 = 3*64 + 8)
+    ((300, 200), 7, 'l1', 'nonneg', (1.0, 1.0)),   # tier 3, L1
+    ((261, 132), 11, 'l21', 'segment', (1.0, 1.0)),  # psf half 5 in tier 7, 4-column last strip
+    ((190, 256), 5, 'l1', '', (2.0, 0.5)),          # psf half 2 in tier 3, non-unit steps
+    ((1000, 128), 15, 'l1', 'segment', (0.5, 1.0)),  # tall: many row segments, short last one
+    ((1000, 4096), 15, 'l21', 'nonneg', (1.0, 1.0)),  # C3 width: 6-step tasks, 3-step last segment
+]
+
+
+@pytest.mark.parametrize('case', range(len(CASES)))
+def test_march_vs_oracle(case):
+    shape, L, hname, gname, steps = CASES[case]
+    p = _problem(shape, L, hname, gname, steps, seed=case)
+    xr, zr, dr, lip = _oracle(p)
+    x, z, diag = _fused(p, lip)
+    assert x.dtype == np.float32
+    assert rel(x, xr) < 5e-5, rel(x, xr)
+    assert rel(z, zr) < 5e-5, rel(z, zr)
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float), dr['primal'],
+                               rtol=2e-2)
+    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float), dr['dual'], rtol=2e-2)
+
+
+def test_march_is_the_kernel_in_use():
+    """The shapes above take the march kernel: one block per (64-column strip, row segment of
+    16-row steps) -- 4 x 19 for 300 x 200 (the tile kernel would launch 4 x 10 tiles of 31 rows)."""
+    import ctypes
+
+    from pycsou_amd import _lib as L
+    a = L.PdsArgs()
+    a.dtype, a.fkind, a.hkind, a.gkind = L.PCS_F32, L.PCS_F_SEPCONV, L.PCS_H_L21, L.PCS_G_NULL
+    a.n0, a.n1, a.row0, a.rows = 300, 200, 0, 300
+    a.half, a.halo_x, a.halo_y, a.halo_z = 7, 0, 0, 0
+    a.step0 = a.step1 = 1.0
+    nb = L.load().pcs_pds2d_nblocks(ctypes.byref(a))
+    assert nb == 4 * 19
