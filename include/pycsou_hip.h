@@ -157,6 +157,10 @@ int pcs_pds2d_halo_x(int half);
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
 int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a);
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
+/* n iterations of pcs_pds2d_step launched back to back, ping-ponging (x, z) <-> (xn, zn)
+ * (even n leaves the iterate in x, z); requires hist/ctrl/ws (in-kernel loop control).  The
+ * host-side form of GenericIterativeAlgorithm.iterate's loop (pycsou/core/solver.py:55-76). */
+int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t stream);
 
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics for 3-D volumes
  * (pycsou/opt/proxalgs.py:343-394), K = Gradient(kind='forward') in 3-D

@@ -78,6 +78,7 @@ _SIGS = {
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
+    'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
     'pcs_pds3d_nblocks': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_ws_bytes': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_step': (_c_int, [ctypes.POINTER(Pds3Args), _vp]),

@@ -293,6 +293,25 @@ int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
   return PCS_EINVAL;
 }
 
+// n consecutive iterations launched back to back from the host (no graph): iteration i reads
+// (x, z) when i is even and (xn, zn) when odd and writes the other pair, so after an even n the
+// iterate is back in (x, z).  Needs the in-kernel loop control (hist): after the stopping rule
+// fires the remaining launches return at once, exactly as in a captured graph.
+int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t st) {
+  if (!a || n < 0 || !a->hist) return PCS_EINVAL;
+  pcs_pds2d_args b = *a;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i % 2) {
+      b.x = a->xn, b.xn = const_cast<void*>(a->x), b.z = a->zn, b.zn = const_cast<void*>(a->z);
+    } else {
+      b.x = a->x, b.xn = a->xn, b.z = a->z, b.zn = a->zn;
+    }
+    const int rc = pcs_pds2d_step(&b, st);
+    if (rc != PCS_OK) return rc;
+  }
+  return PCS_OK;
+}
+
 int64_t pcs_ctrl_bytes(void) { return 64; }
 
 #ifdef PCS_STAMPS

@@ -18,6 +18,7 @@ iteration count is exactly the reference's.
 """
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -31,6 +32,9 @@ from ..func.penalty import L1Norm, L21Norm, SquaredL2Norm
 from ..linop.base import HomothetyMap
 from ..linop.conv import Convolve2DOp
 from ..linop.diff import GradientOp
+
+# images at least this large launch chunks from C instead of replaying a captured graph
+NATIVE_MIN_PIXELS = int(os.environ.get('PCS_NATIVE_MIN_PIXELS', 1 << 20))
 
 
 def _half_loss_data(F):
@@ -148,6 +152,10 @@ class PDS2DEngine:
         self.graph = None
         self.hist = None
         self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        # large images: each chunk is launched back to back from C (pcs_pds2d_run) -- per-launch
+        # host cost is far below the step, and back-to-back launches measured faster than
+        # replaying a captured graph of the same launches; small images keep the graph
+        self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
 
     # one iteration with parity p (reads buffers p, writes 1-p)
     def _iteration(self, p, hist):
@@ -171,6 +179,13 @@ class PDS2DEngine:
         for i in range(self.chunk):
             self._iteration(i % 2, hist)
 
+    def _chunk_native(self, hist):
+        a = self.args
+        a.x, a.xn = self.X[0].data_ptr(), self.X[1].data_ptr()
+        a.z, a.zn = self.Z[0].data_ptr(), self.Z[1].data_ptr()
+        a.hist = hist.data_ptr()
+        L.check(self.lib.pcs_pds2d_run(ctypes.byref(a), self.chunk, L.stream()), 'pcs_pds2d_run')
+
     # ---- fixed-count loop for benchmarking (bench.py): no early stop, optional per-step events
     def prepare_fixed(self, total_iters, chunk):
         """Device state for `total_iters` iterations that never stop early, captured in
@@ -181,13 +196,17 @@ class PDS2DEngine:
         L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(total_iters), int(total_iters), -1.0, 1, hist_len,
                                         L.stream()), 'pcs_ctrl_init2')
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._chunk(self.hist)
-        torch.cuda.synchronize()
+        if not self.native:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._chunk(self.hist)
+            torch.cuda.synchronize()
 
     def replay(self):
-        self.graph.replay()
+        if self.native:
+            self._chunk_native(self.hist)
+        else:
+            self.graph.replay()
 
     def time_step_kernel(self, n, stream=None):
         """Average duration (ms) of the fused step kernel over `n` eager launches, measured
@@ -225,8 +244,8 @@ class PDS2DEngine:
         L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
                                         int(has_dual), int(hist.numel()), L.stream()), 'pcs_ctrl_init2')
         n_chunks = -(-total // self.chunk)
-        if self.use_graph:
-            if self.graph is None:
+        if self.use_graph or self.native:
+            if self.graph is None and not self.native:
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
@@ -234,7 +253,10 @@ class PDS2DEngine:
                 self.graph = g
             pending = []
             for k in range(n_chunks):
-                self.graph.replay()
+                if self.native:
+                    self._chunk_native(hist)
+                else:
+                    self.graph.replay()
                 ev = torch.cuda.Event()
                 self.ctrl_host.copy_(self.ctrl.view(torch.int32)[:2], non_blocking=True)
                 ev.record()

@@ -3,6 +3,7 @@
   eager+events : one event pair per launch (bench.py's kernel_ms)
   eager        : N back-to-back launches, one event pair around all
   graph(c)     : hipGraph of c iterations replayed, one event pair around all replays
+  native(c)    : pcs_pds2d_run launching c iterations back to back from C
 """
 import ctypes
 import os
@@ -22,8 +23,9 @@ def main():
     pds = bench.build_problem(n, n, torch.float32)
     spec = pds._fused_spec()
     N = 100
-    for c in (50, 10, 2):
+    for native, c in ((False, 50), (False, 10), (True, 50), (True, 10), (True, 2)):
         eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+        eng.native = native
         eng.prepare_fixed(4 * N + 10, c)
         for _ in range(20 // c if c < 20 else 1):
             eng.replay()
@@ -33,7 +35,7 @@ def main():
             eng.replay()
         e1.record()
         torch.cuda.synchronize()
-        print(f'graph({c}): {e0.elapsed_time(e1) / N * 1e3:.1f} us/iter', flush=True)
+        print(f'{"native" if native else "graph"}({c}): {e0.elapsed_time(e1) / N * 1e3:.1f} us/iter', flush=True)
     print(f'eager+events: {eng.time_step_kernel(N) * 1e3:.1f} us/launch', flush=True)
     # eager back-to-back (fresh loop state, no events between launches)
     a = eng.args
