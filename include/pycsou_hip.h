@@ -78,6 +78,18 @@ int pcs_conv2d(int dtype, const void* x, void* out, int64_t n0, int64_t n1, cons
 int pcs_conv1d(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps,
                int k, int off, hipStream_t stream);
 
+/* The axis-0 stage of grad F = C^T (C x - y) for a 3-D Convolve1D chain, in one pass
+ * (pycsou/linop/conv.py:20-164 along axis 0, residual of core/map.py:609-610): on sub-volumes
+ * of nsub planes of `plane` elements,
+ *   r[p] = sum_t h[t] t[p + off - t] - y[p]  for p in [img_lo, img_hi) n [0, nsub) (0 elsewhere;
+ *          t = 0 outside [0, nsub)),
+ *   s[q] = sum_t h[k-1-t] r[q + k-1-off - t]  written for q in [q0, q1) only.
+ * = pcs_conv1d(axis 0) + pcs_axpby(1, -1) + pcs_conv1d(axis 0, flipped) with 3 instead of 7
+ * sub-volume passes.  k <= 15. */
+int pcs_conv0_residual_adjoint(int dtype, const void* t, const void* y, void* s, int64_t nsub, int64_t plane,
+                               const void* taps, int k, int off, int64_t img_lo, int64_t img_hi, int64_t q0,
+                               int64_t q1, hipStream_t stream);
+
 /* ---------------------------------------------------------------- prox / functionals */
 
 /* L1Norm.prox (pycsou/func/penalty.py:194-245 via LpNorm.prox, func/base.py:239-240):

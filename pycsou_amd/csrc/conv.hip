@@ -202,28 +202,34 @@ __global__ __launch_bounds__(256) void k_conv1d_strided(const T* __restrict__ x,
   }
 }
 
-// Contiguous axis (stride 1): a block owns a 16*256-byte segment of one row (staged in LDS
-// with a 16-B aligned halo of >= 14 elements each side); thread i computes the 16 B of
-// outputs at 16*i from 16-B LDS reads.  SH = (off + 2*VN - 14) mod VN ... selects the window
-// alignment at compile time.
-template <typename T, int SHIFT>
+// Contiguous axis (stride 1): TPR threads own a TPR*16-byte segment of one row (staged in LDS
+// with a 16-B aligned halo of >= 14 elements each side); a 256-thread block holds 256/TPR such
+// row segments (short rows: several rows per block, no idle lanes).  Thread i of a segment
+// computes the 16 B of outputs at 16*i from 16-B LDS reads.  SHIFT = (16 + off - 14) mod VN
+// selects the window alignment at compile time.
+template <typename T, int SHIFT, int TPR>
 __global__ __launch_bounds__(256) void k_conv1d_contig(const T* __restrict__ x, T* __restrict__ out, int64_t rows,
                                                         int64_t na, const T* __restrict__ taps, int k, int off) {
   constexpr int VN = V16<T>::N;
-  constexpr int SEG = 256 * VN;         // outputs per block
+  constexpr int SEG = TPR * VN;         // outputs per row segment
+  constexpr int RPB = 256 / TPR;        // row segments per block
   constexpr int HALO = 16;              // elements (multiple of VN, >= 14)
+  constexpr int SP = SEG + 2 * HALO + 2 * VN;  // LDS elements per segment
   constexpr int NW = (VN + kC1K - 1 + SHIFT + VN - 1) / VN;  // 16-B reads per window
-  __shared__ __attribute__((aligned(16))) T sm[SEG + 2 * HALO + 2 * VN];
+  __shared__ __attribute__((aligned(16))) T sm[RPB * SP];
   T h[kC1K];
 #pragma unroll
   for (int t = 0; t < kC1K; ++t) h[t] = t < k ? taps[t] : T(0);
   const int64_t nseg = (na + SEG - 1) / SEG;
-  const int64_t r = blockIdx.x / nseg, sgi = blockIdx.x - r * nseg;
-  if (r >= rows) return;
+  const int sub = threadIdx.x / TPR, i = threadIdx.x - sub * TPR;
+  const int64_t task = (int64_t)blockIdx.x * RPB + sub;
+  const int64_t r = task / nseg, sgi = task - r * nseg;
+  const bool live = r < rows;
   const int64_t c0 = sgi * SEG;
-  const T* xr = x + r * na;
+  const T* xr = x + (live ? r : 0) * na;
+  T* ss = sm + sub * SP;
   // stage [c0 - HALO, c0 + SEG + HALO) (zero outside the row), 16 B per thread-load
-  for (int e = threadIdx.x; e < (SEG + 2 * HALO) / VN; e += 256) {
+  for (int e = i; e < (SEG + 2 * HALO) / VN; e += TPR) {
     const int64_t c = c0 - HALO + (int64_t)e * VN;
     V16<T> v;
     if (c >= 0 && c + VN <= na) {
@@ -232,18 +238,18 @@ __global__ __launch_bounds__(256) void k_conv1d_contig(const T* __restrict__ x, 
 #pragma unroll
       for (int q = 0; q < VN; ++q) v.v[q] = (c + q >= 0 && c + q < na) ? xr[c + q] : T(0);
     }
-    stv(sm + e * VN, v);
+    stv(ss + e * VN, v);
   }
   __syncthreads();
+  if (!live) return;
   // outputs j = c0 + VN*i + m read inputs j + off - t, t < 15: LDS index
   // VN*i + m + HALO + off - 14 + (14 - t); window start (aligned) base = VN*i + ((HALO + off - 14) & ~(VN-1))
-  const int i = threadIdx.x;
   const int start = HALO + off - (kC1K - 1);  // >= 2 since off >= 0
   const int abase = VN * i + (start & ~(VN - 1));
   T w[NW * VN];
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
-    const V16<T> v = *reinterpret_cast<const V16<T>*>(sm + abase + q * VN);
+    const V16<T> v = *reinterpret_cast<const V16<T>*>(ss + abase + q * VN);
 #pragma unroll
     for (int e = 0; e < VN; ++e) w[q * VN + e] = v.v[e];
   }
@@ -263,6 +269,93 @@ __global__ __launch_bounds__(256) void k_conv1d_contig(const T* __restrict__ x, 
     for (int m = 0; m < VN; ++m)
       if (j + m < na) out[r * na + j + m] = o.v[m];
   }
+}
+
+template <typename T, int TPR>
+static void launch_contig(const T* x, T* out, int64_t rows, int64_t na, const T* taps, int k, int off, hipStream_t st) {
+  constexpr int VN = V16<T>::N;
+  const int64_t nseg = (na + TPR * VN - 1) / (TPR * VN);
+  const unsigned g = (unsigned)((rows * nseg + 256 / TPR - 1) / (256 / TPR));
+  switch ((16 + off - (kC1K - 1)) & (VN - 1)) {
+    case 0: k_conv1d_contig<T, 0, TPR><<<g, 256, 0, st>>>(x, out, rows, na, taps, k, off); break;
+    case 1: k_conv1d_contig<T, 1, TPR><<<g, 256, 0, st>>>(x, out, rows, na, taps, k, off); break;
+    case 2: k_conv1d_contig<T, 2, TPR><<<g, 256, 0, st>>>(x, out, rows, na, taps, k, off); break;
+    default: k_conv1d_contig<T, 3, TPR><<<g, 256, 0, st>>>(x, out, rows, na, taps, k, off); break;
+  }
+}
+
+template <typename T, int KT>
+__global__ __launch_bounds__(256) void k_conv0_rta(const T* __restrict__ tin, const T* __restrict__ y, T* __restrict__ s,
+                                                   int64_t nsub, int64_t plane, const T* __restrict__ taps, int k,
+                                                   int off, int64_t img_lo, int64_t img_hi, int64_t q0, int64_t q1) {
+  const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pos >= plane) return;
+  T h[KT], hf[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    h[t] = t < k ? taps[t] : T(0);
+    hf[t] = t < k ? taps[k - 1 - t] : T(0);
+  }
+  const int64_t p0 = q0 + k - 2 * KT + 1;  // first plane loaded: both windows full at the first output
+  const int64_t nsteps = (q1 + k - 2) - p0 + 1;
+  const int64_t nblk = (nsteps + KT - 1) / KT;
+  const int64_t lo = img_lo > 0 ? img_lo : 0, hi = img_hi < nsub ? img_hi : nsub;
+  T tw[KT], rw[KT], tl[KT], yl[KT];
+#pragma unroll
+  for (int u = 0; u < KT; ++u) tw[u] = rw[u] = T(0);
+  auto load_blk = [&](int64_t b, T (&tv)[KT], T (&yv)[KT]) {
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const int64_t p = p0 + b * KT + u, pr = p - off;
+      const bool tin_ok = p >= 0 && p < nsub, y_ok = pr >= lo && pr < hi;
+      const T a = tin[(tin_ok ? p : 0) * plane + pos];
+      const T c = y[(y_ok ? pr : lo) * plane + pos];
+      tv[u] = tin_ok ? a : T(0);
+      yv[u] = y_ok ? c : T(0);
+    }
+  };
+  if (nblk > 0) load_blk(0, tl, yl);
+  for (int64_t b = 0; b < nblk; ++b) {
+    T tn[KT], yn[KT];
+    if (b + 1 < nblk) load_blk(b + 1, tn, yn);
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const int64_t p = p0 + b * KT + u, pr = p - off, q = p - k + 1;
+      tw[u] = tl[u];
+      T acc = T(0);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc += h[t] * tw[(u - t + KT) % KT];
+      rw[u] = (pr >= lo && pr < hi) ? acc - yl[u] : T(0);
+      T sacc = T(0);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) sacc += hf[t] * rw[(u - t + KT) % KT];
+      if (q >= q0 && q < q1) s[q * plane + pos] = sacc;
+    }
+    if (b + 1 < nblk) {
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        tl[u] = tn[u];
+        yl[u] = yn[u];
+      }
+    }
+  }
+}
+
+template <typename T>
+static int conv0_rta(const void* t, const void* y, void* s, int64_t nsub, int64_t plane, const void* taps, int k, int off,
+                     int64_t img_lo, int64_t img_hi, int64_t q0, int64_t q1, hipStream_t st) {
+  if (!t || !y || !s || !taps || nsub < 1 || plane < 1 || k < 1 || k > kC1K || off < 0 || off >= k || q0 < 0 ||
+      q1 > nsub || q0 > q1)
+    return PCS_EINVAL;
+  if (q0 == q1) return PCS_OK;
+  const unsigned g = (unsigned)((plane + 255) / 256);
+  if (k <= 7)
+    k_conv0_rta<T, 7><<<g, 256, 0, st>>>((const T*)t, (const T*)y, (T*)s, nsub, plane, (const T*)taps, k, off, img_lo,
+                                         img_hi, q0, q1);
+  else
+    k_conv0_rta<T, kC1K><<<g, 256, 0, st>>>((const T*)t, (const T*)y, (T*)s, nsub, plane, (const T*)taps, k, off,
+                                            img_lo, img_hi, q0, q1);
+  return launch_status();
 }
 
 template <typename T>
@@ -286,16 +379,14 @@ static int conv1d(const void* x, void* out, int ndim, const int64_t* dims, int a
   }
   if (k <= kC1K && al && sa == 1 && dims[axis] % VN == 0) {
     const int64_t rows = outer, na = dims[axis];
-    const int64_t nseg = (na + 256 * VN - 1) / (256 * VN);
-    if (rows * nseg < (1LL << 31)) {
-      const int s = (16 + off - (kC1K - 1)) & (VN - 1);
-      const unsigned g = (unsigned)(rows * nseg);
-      switch (s) {
-        case 0: k_conv1d_contig<T, 0><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
-        case 1: k_conv1d_contig<T, 1><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
-        case 2: k_conv1d_contig<T, 2><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
-        default: k_conv1d_contig<T, 3><<<g, 256, 0, st>>>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off); break;
-      }
+    if (rows * ((na + VN * 64 - 1) / (VN * 64)) < (1LL << 31)) {
+      // threads per row segment: the fewest (64 / 128 / 256) that cover the row, else 256
+      if (na <= 64 * VN)
+        launch_contig<T, 64>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off, st);
+      else if (na <= 128 * VN)
+        launch_contig<T, 128>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off, st);
+      else
+        launch_contig<T, 256>((const T*)x, (T*)out, rows, na, (const T*)taps, k, off, st);
       return launch_status();
     }
   }
@@ -313,6 +404,14 @@ int pcs_conv2d(int dt, const void* x, void* out, int64_t n0, int64_t n1, const v
                int off1, const void* b, double beta, hipStream_t st) {
   if (dt == PCS_F32) return conv2d<float>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
   if (dt == PCS_F64) return conv2d<double>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
+  return PCS_EINVAL;
+}
+
+int pcs_conv0_residual_adjoint(int dt, const void* t, const void* y, void* s, int64_t nsub, int64_t plane,
+                               const void* taps, int k, int off, int64_t img_lo, int64_t img_hi, int64_t q0, int64_t q1,
+                               hipStream_t st) {
+  if (dt == PCS_F32) return conv0_rta<float>(t, y, s, nsub, plane, taps, k, off, img_lo, img_hi, q0, q1, st);
+  if (dt == PCS_F64) return conv0_rta<double>(t, y, s, nsub, plane, taps, k, off, img_lo, img_hi, q0, q1, st);
   return PCS_EINVAL;
 }
 

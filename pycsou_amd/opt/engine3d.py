@@ -9,8 +9,12 @@ Problem family (what a reference script builds for 3-D TV deconvolution / denois
 
 One iteration of ``PrimalDualSplitting`` (``pycsou/opt/proxalgs.py:343-394``):
 
-    g = C^T (C x - y)          pcs_conv1d per axis (forward chain), pcs_axpby, the flipped
-                               chain (exactly the reference's Conv^T((2 (Conv x - y)) 0.5))
+    g = C^T (C x - y)          in-plane pcs_conv1d passes, then pcs_conv0_residual_adjoint (the
+                               axis-0 conv, the residual (C x) + (-y) and the axis-0 adjoint in
+                               one plane-streaming pass), then the in-plane adjoint passes on the
+                               planes the update reads (the reference's Conv^T((2 (Conv x - y)) 0.5)
+                               with the separable passes regrouped); other chains: pcs_conv1d per
+                               axis, pcs_axpby, the flipped chain
     pcs_pds3d_step             x, z, g -> x', z', norm partials, loop control
 
 Volumes are split into slabs of planes (axis 0) across ranks exactly like the 2-D rows of
@@ -135,8 +139,21 @@ class PDS3DEngine:
             # planes of the sub-volume outside the image: the residual is 0 there
             self.zero_planes = [j for j in range(self.rows + 2 * hx)
                                 if not 0 <= self.row0 - hx + j < n0]
-            # the chain's final buffer is fixed by its length: forward + adjoint passes
-            self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
+            ax0 = [c for c in self.chain if c[0] == 0]
+            # one axis-0 Convolve1D of <= 15 taps: in-plane passes, then the axis-0 forward conv,
+            # residual and adjoint conv fused in one plane-streaming pass, then the in-plane
+            # adjoint passes on the planes the update reads only
+            self.fused0 = len(ax0) == 1 and ax0[0][3] <= 15
+            if self.fused0:
+                self.inplane = [c for c in self.chain if c[0] != 0]
+                self.ax0 = ax0[0]
+                nin = len(self.inplane)
+                # forward passes alternate T0/T1 from x, the fused pass and the adjoint passes
+                # continue the alternation: 2 nin + 1 passes end in T[(2 nin) % 2]
+                self.gbuf = self.T[(2 * nin) % 2]
+            else:
+                # the chain's final buffer is fixed by its length: forward + adjoint passes
+                self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
         a = L.Pds3Args()
         a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
         a.fkind, a.hkind, a.gkind = fk, spec['hkind'], spec['gkind']
@@ -180,7 +197,36 @@ class PDS3DEngine:
         L.check(self.lib.pcs_conv1d(self.base_args.dtype, L.ptr(src), L.ptr(dst), 3, L.i64s(self.sub_dims),
                                     int(axis), L.ptr(taps), int(k), int(off), st), 'pcs_conv1d')
 
+    def _gradient_fused0(self, p, st):
+        nsub = self.rows + 2 * self.hx
+        plane = self.plane
+        cur, j = self.X[p], 0
+        for axis, h, _, k, off in self.inplane:
+            dst = self.T[j % 2]
+            self._conv_into(cur, dst, axis, h, k, off, st)
+            cur, j = dst, j + 1
+        # s on the planes the update reads: own planes + the next one (u on the slab's last plane + 1)
+        q0, q1 = self.hx, min(self.hx + self.rows + 1, nsub)
+        img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0
+        _, h, _, k, off = self.ax0
+        dst = self.T[j % 2]
+        L.check(self.lib.pcs_conv0_residual_adjoint(self.base_args.dtype, L.ptr(cur), L.ptr(self.yw), L.ptr(dst), nsub,
+                                                    plane, L.ptr(h), int(k), int(off), img_lo, img_hi, q0, q1, st),
+                'pcs_conv0_residual_adjoint')
+        cur, j = dst, j + 1
+        dims = L.i64s((q1 - q0, self.n1, self.n2))
+        esz = cur.element_size()
+        for axis, _, hf, k, off in reversed(self.inplane):
+            dst = self.T[j % 2]
+            L.check(self.lib.pcs_conv1d(self.base_args.dtype, ctypes.c_void_p(cur.data_ptr() + q0 * plane * esz),
+                                        ctypes.c_void_p(dst.data_ptr() + q0 * plane * esz), 3, dims, int(axis),
+                                        L.ptr(hf), int(k), int(k - 1 - off), st), 'pcs_conv1d')
+            cur, j = dst, j + 1
+        assert cur is self.gbuf
+
     def _gradient(self, p, st):
+        if self.fused0:
+            return self._gradient_fused0(p, st)
         cur, j = self.X[p], 0
         for axis, h, _, k, off in self.chain:
             dst = self.T[j % 2]

@@ -1,0 +1,96 @@
+"""2-D PDS throughput on one GPU for the other 2-D configs:
+
+  C2     2048^2 fp32 TV denoising: y = x* + 0.1 N(0,1), H = 0.1 * L21Norm, no blur
+  C3-L1  4096^2 fp32 TV-deconvolution with the anisotropic 0.05 * L1Norm
+
+Built through the public API, run by PDS2DEngine (fixed iteration count).  Prints one JSON
+line per config: it/s, us per iteration, algorithmic GB/s (7 N words per iteration) and the
+fraction of 8 TB/s.
+
+  python tools/bench2d.py --steps 500 --warmup 50
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def c2(n=2048, seed=0):
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    N = n * n
+    xs = torch.as_tensor(bench.phantom((n, n), 64, seed).ravel()).to('cuda', torch.float32)
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = xs + 0.1 * torch.randn(N, generator=g, device='cuda', dtype=torch.float32)
+    K = Gradient(shape=(n, n), kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(8 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y)
+    H = 0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2))
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, device='cuda'), z0=torch.zeros(2 * N, device='cuda'),
+               verbose=None)
+
+
+def c3_l1(n=4096, seed=0):
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L1Norm
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    N = n * n
+    xs = torch.as_tensor(bench.phantom((n, n), 64, seed).ravel()).to('cuda', torch.float32)
+    C = Convolve2D(size=N, filter=bench.gaussian_psf(15, 2.0), shape=(n, n))
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = C(xs) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=torch.float32)
+    K = Gradient(shape=(n, n), kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(8 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    return PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y) * C, H=0.05 * L1Norm(dim=2 * N), K=K,
+               x0=torch.zeros(N, device='cuda'), z0=torch.zeros(2 * N, device='cuda'), verbose=None)
+
+
+def run(name, pds, n, K, W):
+    from pycsou_amd.opt.engine import PDS2DEngine
+    spec = pds._fused_spec()
+    assert spec is not None
+    eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    chunk = 50
+    eng.prepare_fixed(W + K + 4, chunk)
+    bench.spin_up(eng, 50)
+    eng.prepare_fixed(W + K + 4, chunk)
+    for _ in range(W // chunk):
+        eng.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(K // chunk):
+        eng.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / K
+    alg = 7 * n * n * 4
+    print(json.dumps({'config': name, 'it_per_s': round(1e3 / ms, 1), 'us_per_iter': round(ms * 1e3, 2),
+                      'alg_GBps': round(alg / (ms * 1e-3) / 1e9, 1), 'frac_of_8TBps': round(alg / (ms * 1e-3) / 8e12, 4),
+                      'native_launch': bool(eng.native), 'nblocks': eng.nblocks}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=500)
+    ap.add_argument('--warmup', type=int, default=50)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    K, W = args.steps // 50 * 50, args.warmup // 50 * 50
+    run('C2 2048^2 fp32 TV denoising (0.1*L21)', c2(), 2048, K, W)
+    run('C3 4096^2 fp32 TV-deconvolution, anisotropic 0.05*L1', c3_l1(), 4096, K, W)
+
+
+if __name__ == '__main__':
+    main()
