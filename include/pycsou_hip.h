@@ -78,6 +78,14 @@ int pcs_conv2d(int dtype, const void* x, void* out, int64_t n0, int64_t n1, cons
 int pcs_conv1d(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps,
                int k, int off, hipStream_t stream);
 
+/* Two Convolve1D of a 3-D array's planes in one pass (pycsou/linop/conv.py:20-164 along axes 1
+ * and 2): C_a along axis 1 (taps ha, ka, offa), C_b along axis 2 (taps hb, kb, offb), both with
+ * pcs_conv1d's definition; out = C_b(C_a(in)) if vfirst else C_a(C_b(in)) (the two pcs_conv1d
+ * calls in that order, same per-output sums to rounding).  in != out, 16-B aligned; ka, kb <= 15. */
+int pcs_conv2d_sep_planes(int dtype, const void* in, void* out, int64_t nplanes, int64_t n1, int64_t n2,
+                          const void* ha, int ka, int offa, const void* hb, int kb, int offb, int vfirst,
+                          hipStream_t stream);
+
 /* The axis-0 stage of grad F = C^T (C x - y) for a 3-D Convolve1D chain, in one pass
  * (pycsou/linop/conv.py:20-164 along axis 0, residual of core/map.py:609-610): on sub-volumes
  * of nsub planes of `plane` elements,

@@ -358,6 +358,215 @@ static int conv0_rta(const void* t, const void* y, void* s, int64_t nsub, int64_
   return launch_status();
 }
 
+// ---- two Convolve1D along axes 1 and 2 of every plane of a 3-D array in one pass
+// (the in-plane part of a separable 3-D blur, pycsou/linop/conv.py:20-164):
+//   VFIRST:  out = C_b(C_a(in)),   !VFIRST: out = C_a(C_b(in)),
+// C_a along axis 1 (taps ha, ka, offa), C_b along axis 2 (taps hb, kb, offb), zero boundary.
+// A block computes a TY x 64 tile of one plane: the input tile with its halo (TY + 14 rows,
+// 64 + 32 columns, zeros outside the plane) is staged in LDS once, the first pass writes an LDS
+// intermediate, the second pass writes the output: 2 sub-volume passes instead of 4.  Each
+// output is the same t-ascending sum as pcs_conv1d's.
+template <typename T>
+struct Q4 {
+  T v[4];
+};
+template <typename T>
+__device__ __forceinline__ Q4<T> ldq(const T* p) {  // 4 elements, 16-B aligned
+  Q4<T> r;
+  constexpr int VN = V16<T>::N;
+#pragma unroll
+  for (int h = 0; h < 4 / VN; ++h) {
+    const V16<T> v = ldv(p + h * VN);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) r.v[h * VN + e] = v.v[e];
+  }
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void stq(T* p, const Q4<T>& r) {
+  constexpr int VN = V16<T>::N;
+#pragma unroll
+  for (int h = 0; h < 4 / VN; ++h) {
+    V16<T> v;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) v.v[e] = r.v[h * VN + e];
+    stv(p + h * VN, v);
+  }
+}
+
+template <typename T>
+struct Sep2D {
+  static constexpr int KT = kC1K, TX = 64, CH = 16, WC = TX + 2 * CH, GC = WC / 4;
+  static constexpr int TY = sizeof(T) == 4 ? 32 : 16, NR = TY + KT - 1;
+};
+
+template <typename T, int SHIFT, bool VFIRST>
+__global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __restrict__ out, int64_t nplanes, int64_t n1,
+                                               int64_t n2, const T* __restrict__ ha_, int ka, int offa,
+                                               const T* __restrict__ hb_, int kb, int offb) {
+  using S = Sep2D<T>;
+  constexpr int KT = S::KT, TX = S::TX, CH = S::CH, WC = S::WC, GC = S::GC, TY = S::TY, NR = S::NR;
+  constexpr int SZ_IN = NR * WC, SZ_MID = VFIRST ? TY * WC : NR * TX;
+  __shared__ __attribute__((aligned(16))) T sm[SZ_IN + SZ_MID];
+  T* tin = sm;
+  T* mid = sm + SZ_IN;
+  T ha[KT], hb[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    ha[t] = t < ka ? ha_[t] : T(0);
+    hb[t] = t < kb ? hb_[t] : T(0);
+  }
+  const int64_t ty = (n1 + TY - 1) / TY, tx = (n2 + TX - 1) / TX;
+  const int64_t b = blockIdx.x;
+  const int64_t pl = b / (ty * tx), rem = b - pl * (ty * tx);
+  const int64_t i0 = (rem / tx) * TY, j0 = (rem - (rem / tx) * tx) * TX;
+  const T* src = in + pl * n1 * n2;
+  T* dst = out + pl * n1 * n2;
+  const int tid = threadIdx.x;
+  const bool vec = (n2 % 4 == 0);
+  // stage rows [i0 + offa - 14, i0 + TY + offa), columns [j0 - 16, j0 + 80): all of a
+  // thread's loads are issued before its LDS stores
+  constexpr int NL = (NR * GC + 255) / 256;
+  Q4<T> q[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int e = min(l * 256 + tid, NR * GC - 1);
+    const int rl = e / GC, g = e - (e / GC) * GC;
+    const int64_t gi = i0 + offa - (KT - 1) + rl, gc = j0 - CH + 4 * g;
+    const bool rin = gi >= 0 && gi < n1;
+    if (rin && vec && gc >= 0 && gc + 4 <= n2) {
+      q[l] = ldq(src + gi * n2 + gc);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[l].v[m] = (rin && gc + m >= 0 && gc + m < n2) ? src[gi * n2 + gc + m] : T(0);
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int e = l * 256 + tid;
+    if (e < NR * GC) stq(tin + (e / GC) * WC + 4 * (e - (e / GC) * GC), q[l]);
+  }
+  __syncthreads();
+  // horizontal window: outputs at tile column c (multiple of 4) read tile columns
+  // c + CH + offb - 14 + (14 - t); aligned start c + ((CH + offb - 14) & ~3), SHIFT the rest
+  constexpr int NW = (4 + KT - 1 + SHIFT + 3) / 4;
+  const int hb0 = (CH + offb - (KT - 1)) & ~3;
+  auto hpass = [&](const T* row, int c, Q4<T>& o) {  // row: LDS row base; c: first output col in the row's frame
+    T w[NW * 4];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const Q4<T> v = ldq(row + c + hb0 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[4 * q + e] = v.v[e];
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      T acc = T(0);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc += hb[t] * w[SHIFT + m + (KT - 1 - t)];
+      o.v[m] = acc;
+    }
+  };
+  // vertical: output row i (tile frame) = sum_t ha[t] rows[i + 14 - t] of a NR-row buffer
+  constexpr int RB = 4;
+  // each of the RB + 14 rows is read once; rows from the bottom up = t ascending per output
+  auto vpass = [&](const T* buf, int pitch, int i, int c, Q4<T> (&acc)[RB]) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
+#pragma unroll
+    for (int j = RB + KT - 2; j >= 0; --j) {
+      const Q4<T> v = ldq(buf + (i + j) * pitch + c);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int t = r + KT - 1 - j;
+        if (t >= 0 && t < KT) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
+        }
+      }
+    }
+  };
+  auto store = [&](int i, int c, const Q4<T>& o) {  // tile row i, tile col c (multiple of 4)
+    const int64_t gi = i0 + i, gc = j0 + c;
+    if (gi >= n1) return;
+    if (vec && gc + 4 <= n2) {
+      stq(dst + gi * n2 + gc, o);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (gc + m < n2) dst[gi * n2 + gc + m] = o.v[m];
+    }
+  };
+  if (VFIRST) {
+    // mid[i][c] (i < TY, all WC columns) = vertical pass
+    for (int e = tid; e < (TY / RB) * GC; e += 256) {
+      const int rb = e / GC, g = e - (e / GC) * GC;
+      Q4<T> acc[RB];
+      vpass(tin, WC, rb * RB, 4 * g, acc);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) stq(mid + (rb * RB + r) * WC + 4 * g, acc[r]);
+    }
+    __syncthreads();
+    for (int e = tid; e < TY * (TX / 4); e += 256) {
+      const int i = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
+      Q4<T> o;
+      hpass(mid + i * WC, 4 * g, o);
+      store(i, 4 * g, o);
+    }
+  } else {
+    // mid[r][c] (all NR rows, TX columns) = horizontal pass
+    for (int e = tid; e < NR * (TX / 4); e += 256) {
+      const int r = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
+      Q4<T> o;
+      hpass(tin + r * WC, 4 * g, o);
+      stq(mid + r * TX + 4 * g, o);
+    }
+    __syncthreads();
+    for (int e = tid; e < (TY / RB) * (TX / 4); e += 256) {
+      const int rb = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
+      Q4<T> acc[RB];
+      vpass(mid, TX, rb * RB, 4 * g, acc);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) store(rb * RB + r, 4 * g, acc[r]);
+    }
+  }
+}
+
+template <typename T, bool VFIRST>
+static void launch_sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
+                         const void* hb, int kb, int offb, hipStream_t st) {
+  using S = Sep2D<T>;
+  const unsigned g = (unsigned)(np * ((n1 + S::TY - 1) / S::TY) * ((n2 + S::TX - 1) / S::TX));
+  auto args = [&](auto kern) {
+    kern<<<g, 256, 0, st>>>((const T*)in, (T*)out, np, n1, n2, (const T*)ha, ka, offa, (const T*)hb, kb, offb);
+  };
+  switch ((S::CH + offb - (S::KT - 1)) & 3) {
+    case 0: args(k_sep2d<T, 0, VFIRST>); break;
+    case 1: args(k_sep2d<T, 1, VFIRST>); break;
+    case 2: args(k_sep2d<T, 2, VFIRST>); break;
+    default: args(k_sep2d<T, 3, VFIRST>); break;
+  }
+}
+
+template <typename T>
+static int sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
+                 const void* hb, int kb, int offb, int vfirst, hipStream_t st) {
+  using S = Sep2D<T>;
+  if (!in || !out || !ha || !hb || np < 0 || n1 < 1 || n2 < 1 || ka < 1 || ka > kC1K || kb < 1 || kb > kC1K || offa < 0 ||
+      offa >= ka || offb < 0 || offb >= kb || in == out)
+    return PCS_EINVAL;
+  if ((uintptr_t)in % 16 || (uintptr_t)out % 16) return PCS_EINVAL;
+  if (np == 0) return PCS_OK;
+  if (np * ((n1 + S::TY - 1) / S::TY) * ((n2 + S::TX - 1) / S::TX) >= (1LL << 31)) return PCS_EUNSUPPORTED;
+  if (vfirst)
+    launch_sep2d<T, true>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
+  else
+    launch_sep2d<T, false>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
+  return launch_status();
+}
+
 template <typename T>
 static int conv1d(const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps, int k, int off,
                   hipStream_t st) {
@@ -404,6 +613,13 @@ int pcs_conv2d(int dt, const void* x, void* out, int64_t n0, int64_t n1, const v
                int off1, const void* b, double beta, hipStream_t st) {
   if (dt == PCS_F32) return conv2d<float>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
   if (dt == PCS_F64) return conv2d<double>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
+  return PCS_EINVAL;
+}
+
+int pcs_conv2d_sep_planes(int dt, const void* in, void* out, int64_t nplanes, int64_t n1, int64_t n2, const void* ha,
+                          int ka, int offa, const void* hb, int kb, int offb, int vfirst, hipStream_t st) {
+  if (dt == PCS_F32) return sep2d<float>(in, out, nplanes, n1, n2, ha, ka, offa, hb, kb, offb, vfirst, st);
+  if (dt == PCS_F64) return sep2d<double>(in, out, nplanes, n1, n2, ha, ka, offa, hb, kb, offb, vfirst, st);
   return PCS_EINVAL;
 }
 

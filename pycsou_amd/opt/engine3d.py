@@ -150,7 +150,11 @@ class PDS3DEngine:
                 nin = len(self.inplane)
                 # forward passes alternate T0/T1 from x, the fused pass and the adjoint passes
                 # continue the alternation: 2 nin + 1 passes end in T[(2 nin) % 2]
-                self.gbuf = self.T[(2 * nin) % 2]
+                self.gbuf = self.T[0]
+                # one axis-1 and one axis-2 conv of <= 15 taps: both in-plane passes in one launch
+                esz = torch.empty(0, dtype=dtype).element_size()
+                self.sep2 = (sorted(c[0] for c in self.inplane) == [1, 2] and all(c[3] <= 15 for c in self.inplane)
+                             and (plane * esz) % 16 == 0)
             else:
                 # the chain's final buffer is fixed by its length: forward + adjoint passes
                 self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
@@ -197,14 +201,28 @@ class PDS3DEngine:
         L.check(self.lib.pcs_conv1d(self.base_args.dtype, L.ptr(src), L.ptr(dst), 3, L.i64s(self.sub_dims),
                                     int(axis), L.ptr(taps), int(k), int(off), st), 'pcs_conv1d')
 
+    def _sep_planes(self, src, dst, np_, ops, flipped, st):
+        """Both in-plane passes of `ops` (axis 1 and axis 2, application order) in one launch."""
+        (a0, h0, hf0, k0, o0), (a1, h1, hf1, k1, o1) = ops
+        first, second = (h0, k0, o0) if not flipped else (hf0, k0, k0 - 1 - o0), \
+                        (h1, k1, o1) if not flipped else (hf1, k1, k1 - 1 - o1)
+        (ha, ka, oa), (hb, kb, ob) = (first, second) if a0 == 1 else (second, first)
+        L.check(self.lib.pcs_conv2d_sep_planes(self.base_args.dtype, src, dst, np_, self.n1, self.n2, L.ptr(ha), ka, oa,
+                                               L.ptr(hb), kb, ob, int(a0 == 1), st), 'pcs_conv2d_sep_planes')
+
     def _gradient_fused0(self, p, st):
         nsub = self.rows + 2 * self.hx
         plane = self.plane
         cur, j = self.X[p], 0
-        for axis, h, _, k, off in self.inplane:
-            dst = self.T[j % 2]
-            self._conv_into(cur, dst, axis, h, k, off, st)
-            cur, j = dst, j + 1
+        if self.sep2:
+            dst = self.T[0]
+            self._sep_planes(L.ptr(cur), L.ptr(dst), nsub, self.inplane, False, st)
+            cur, j = dst, 1
+        else:
+            for axis, h, _, k, off in self.inplane:
+                dst = self.T[j % 2]
+                self._conv_into(cur, dst, axis, h, k, off, st)
+                cur, j = dst, j + 1
         # s on the planes the update reads: own planes + the next one (u on the slab's last plane + 1)
         q0, q1 = self.hx, min(self.hx + self.rows + 1, nsub)
         img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0
@@ -216,6 +234,13 @@ class PDS3DEngine:
         cur, j = dst, j + 1
         dims = L.i64s((q1 - q0, self.n1, self.n2))
         esz = cur.element_size()
+        if self.sep2:
+            dst = self.T[j % 2]
+            self._sep_planes(ctypes.c_void_p(cur.data_ptr() + q0 * plane * esz),
+                             ctypes.c_void_p(dst.data_ptr() + q0 * plane * esz), q1 - q0, self.inplane[::-1], True, st)
+            cur = dst
+            assert cur is self.gbuf
+            return
         for axis, _, hf, k, off in reversed(self.inplane):
             dst = self.T[j % 2]
             L.check(self.lib.pcs_conv1d(self.base_args.dtype, ctypes.c_void_p(cur.data_ptr() + q0 * plane * esz),

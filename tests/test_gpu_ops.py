@@ -173,6 +173,30 @@ def test_conv0_residual_adjoint(A, dtype, k, off, nsub, img, q):
     assert rel(got[q[0]:q[1]], s_ref[q[0]:q[1]]) < 10 * TOL[dtype]
 
 
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('ka,offa,kb,offb', [(15, 7, 15, 7), (7, 3, 5, 2), (4, 1, 12, 9), (1, 0, 15, 14)])
+@pytest.mark.parametrize('dims', [(3, 40, 72), (2, 33, 130), (1, 5, 7)])
+@pytest.mark.parametrize('vfirst', [1, 0])
+def test_conv2d_sep_planes(A, dtype, ka, offa, kb, offb, dims, vfirst):
+    """pcs_conv2d_sep_planes == the two pcs_conv1d passes (axis 1, axis 2) in the same order,
+    bit for bit (same per-output sums); odd widths take the scalar staging path."""
+    from pycsou_amd import _lib as L
+    rng = np.random.default_rng(ka * 31 + kb)
+    x = dev(rng.standard_normal(dims).astype(dtype))
+    ha, hb = dev(rng.standard_normal(ka).astype(dtype)), dev(rng.standard_normal(kb).astype(dtype))
+    lib, st = L.load(), L.stream()
+    t1, ref, out = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+    d = L.i64s(dims)
+    order = [(1, ha, ka, offa), (2, hb, kb, offb)] if vfirst else [(2, hb, kb, offb), (1, ha, ka, offa)]
+    (a0, h0, k0, o0), (a1, h1, k1, o1) = order
+    assert lib.pcs_conv1d(L.dtcode(x), L.ptr(x), L.ptr(t1), 3, d, a0, L.ptr(h0), k0, o0, st) == 0
+    assert lib.pcs_conv1d(L.dtcode(x), L.ptr(t1), L.ptr(ref), 3, d, a1, L.ptr(h1), k1, o1, st) == 0
+    assert lib.pcs_conv2d_sep_planes(L.dtcode(x), L.ptr(x), L.ptr(out), dims[0], dims[1], dims[2], L.ptr(ha), ka,
+                                     offa, L.ptr(hb), kb, offb, vfirst, st) == 0
+    torch.cuda.synchronize()
+    assert rel(host(out), host(ref)) < TOL[dtype]
+
+
 def test_separable_factorisation(A):
     from pycsou_amd.linop.conv import Convolve2D
     for (kh, kw) in [(15, 15), (4, 6), (7, 3)]:
