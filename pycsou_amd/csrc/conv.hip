@@ -249,7 +249,13 @@ __global__ __launch_bounds__(256) void k_conv1d_contig(const T* __restrict__ x, 
   T w[NW * VN];
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
-    const V16<T> v = *reinterpret_cast<const V16<T>*>(ss + abase + q * VN);
+    V16<T> v;  // whole ds_read_b128 (volatile LDS read: no narrowing into ds_read2_b32)
+    {
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) const volatile u4* lds_u4;
+      const u4 raw = *(lds_u4)(ss + abase + q * VN);
+      __builtin_memcpy(v.v, &raw, 16);
+    }
 #pragma unroll
     for (int e = 0; e < VN; ++e) w[q * VN + e] = v.v[e];
   }
@@ -382,6 +388,22 @@ __device__ __forceinline__ Q4<T> ldq(const T* p) {  // 4 elements, 16-B aligned
   }
   return r;
 }
+// LDS read of 4 elements that stays whole 16-B ds_read_b128 (volatile, LDS address space):
+// otherwise hipcc narrows a read whose edge elements are unused into ds_read2_b32 pairs
+// (32-bank, 2-4 way conflicts)
+template <typename T>
+__device__ __forceinline__ Q4<T> ldsq(const T* p) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const volatile u4* lds_u4;
+  Q4<T> r;
+  constexpr int VN = V16<T>::N;
+#pragma unroll
+  for (int h = 0; h < 4 / VN; ++h) {
+    const u4 v = ((lds_u4)(p))[h];
+    __builtin_memcpy(r.v + h * VN, &v, 16);
+  }
+  return r;
+}
 template <typename T>
 __device__ __forceinline__ void stq(T* p, const Q4<T>& r) {
   constexpr int VN = V16<T>::N;
@@ -394,13 +416,37 @@ __device__ __forceinline__ void stq(T* p, const Q4<T>& r) {
   }
 }
 
+constexpr int64_t kSep2DBlocks = 1024;
+
+// vertical pass over an LDS buffer: acc[r] = sum_t ha[t] rows[i + r + KT - 1 - t] at column c;
+// each of the RB + KT - 1 rows is read once, bottom up (t ascending per output, as pcs_conv1d)
+template <typename T, int RB, int KT>
+__device__ __forceinline__ void sep_vpass(const T* buf, int pitch, int i, int c, const T (&ha)[KT], Q4<T> (&acc)[RB]) {
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
+#pragma unroll
+  for (int j = RB + KT - 2; j >= 0; --j) {
+    const Q4<T> v = ldsq(buf + (i + j) * pitch + c);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int t = r + KT - 1 - j;
+      if (t >= 0 && t < KT) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
+      }
+    }
+  }
+}
+
 template <typename T>
 struct Sep2D {
   static constexpr int KT = kC1K, TX = 64, CH = 16, WC = TX + 2 * CH, GC = WC / 4;
   static constexpr int TY = sizeof(T) == 4 ? 32 : 16, NR = TY + KT - 1;
 };
 
-template <typename T, int SHIFT, bool VFIRST>
+template <typename T, int SHIFT, bool VFIRST, bool VEC>
 __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __restrict__ out, int64_t nplanes, int64_t n1,
                                                int64_t n2, const T* __restrict__ ha_, int ka, int offa,
                                                const T* __restrict__ hb_, int kb, int offb) {
@@ -416,37 +462,48 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
     ha[t] = t < ka ? ha_[t] : T(0);
     hb[t] = t < kb ? hb_[t] : T(0);
   }
-  const int64_t ty = (n1 + TY - 1) / TY, tx = (n2 + TX - 1) / TX;
-  const int64_t b = blockIdx.x;
-  const int64_t pl = b / (ty * tx), rem = b - pl * (ty * tx);
-  const int64_t i0 = (rem / tx) * TY, j0 = (rem - (rem / tx) * tx) * TX;
-  const T* src = in + pl * n1 * n2;
-  T* dst = out + pl * n1 * n2;
+  const int64_t ty = (n1 + TY - 1) / TY, tx = (n2 + TX - 1) / TX, ntiles = nplanes * ty * tx;
   const int tid = threadIdx.x;
-  const bool vec = (n2 % 4 == 0);
-  // stage rows [i0 + offa - 14, i0 + TY + offa), columns [j0 - 16, j0 + 80): all of a
-  // thread's loads are issued before its LDS stores
+  constexpr bool vec = VEC;
+  // persistent blocks: tile b + gridDim.x's input is loaded into registers while tile b computes
+  // stage rows [i0 + offa - 14, i0 + TY + offa), columns [j0 - 16, j0 + 80)
   constexpr int NL = (NR * GC + 255) / 256;
   Q4<T> q[NL];
+  // tile b: plane b / (ty tx), then column strip, row tile fastest (vertical neighbours, which
+  // share 14 halo rows, are consecutive)
+  auto tile_of = [&](int64_t b, int64_t& pl, int64_t& i0, int64_t& j0) {
+    pl = b / (ty * tx);
+    const int64_t rem = b - pl * (ty * tx), sj = rem / ty;
+    i0 = (rem - sj * ty) * TY;
+    j0 = sj * TX;
+  };
+  auto load_tile = [&](int64_t b) {
+    int64_t pl, i0, j0;
+    tile_of(b, pl, i0, j0);
+    const T* src = in + pl * n1 * n2;
 #pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    const int e = min(l * 256 + tid, NR * GC - 1);
-    const int rl = e / GC, g = e - (e / GC) * GC;
-    const int64_t gi = i0 + offa - (KT - 1) + rl, gc = j0 - CH + 4 * g;
-    const bool rin = gi >= 0 && gi < n1;
-    if (rin && vec && gc >= 0 && gc + 4 <= n2) {
-      q[l] = ldq(src + gi * n2 + gc);
-    } else {
+    for (int l = 0; l < NL; ++l) {
+      const int e = min(l * 256 + tid, NR * GC - 1);
+      const int rl = e / GC, g = e - (e / GC) * GC;
+      const int64_t gi = i0 + offa - (KT - 1) + rl, gc = j0 - CH + 4 * g;
+      const bool rin = gi >= 0 && gi < n1;
+      // branch-free (clamped address + select): a load inside a divergent branch makes the
+      // compiler wait for it before the next one is issued
+      if (VEC) {
+        const bool ok = rin && gc >= 0 && gc + 4 <= n2;
+        const Q4<T> v = ldq(src + (ok ? gi * n2 + gc : 0));
 #pragma unroll
-      for (int m = 0; m < 4; ++m) q[l].v[m] = (rin && gc + m >= 0 && gc + m < n2) ? src[gi * n2 + gc + m] : T(0);
+        for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
+      } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const bool ok = rin && gc + m >= 0 && gc + m < n2;
+          const T v = src[ok ? gi * n2 + gc + m : 0];
+          q[l].v[m] = ok ? v : T(0);
+        }
+      }
     }
-  }
-#pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    const int e = l * 256 + tid;
-    if (e < NR * GC) stq(tin + (e / GC) * WC + 4 * (e - (e / GC) * GC), q[l]);
-  }
-  __syncthreads();
+  };
   // horizontal window: outputs at tile column c (multiple of 4) read tile columns
   // c + CH + offb - 14 + (14 - t); aligned start c + ((CH + offb - 14) & ~3), SHIFT the rest
   constexpr int NW = (4 + KT - 1 + SHIFT + 3) / 4;
@@ -454,10 +511,10 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
   auto hpass = [&](const T* row, int c, Q4<T>& o) {  // row: LDS row base; c: first output col in the row's frame
     T w[NW * 4];
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const Q4<T> v = ldq(row + c + hb0 + 4 * q);
+    for (int u = 0; u < NW; ++u) {
+      const Q4<T> v = ldsq(row + c + hb0 + 4 * u);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) w[4 * q + e] = v.v[e];
+      for (int e = 0; e < 4; ++e) w[4 * u + e] = v.v[e];
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -467,69 +524,73 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
       o.v[m] = acc;
     }
   };
-  // vertical: output row i (tile frame) = sum_t ha[t] rows[i + 14 - t] of a NR-row buffer
-  constexpr int RB = 4;
-  // each of the RB + 14 rows is read once; rows from the bottom up = t ascending per output
-  auto vpass = [&](const T* buf, int pitch, int i, int c, Q4<T> (&acc)[RB]) {
+  // LDS lane maps: every 16-lane ds_read_b128 group reads 16 distinct 16-B slots of one row
+  const int half = tid >> 5, l5 = tid & 31, lgrp = lane_grp(l5), lidx = lane_idx(l5);
+  // XCD-aware persistent schedule: the blocks of one XCD (b % 8) walk one contiguous eighth of
+  // the tile order together, so halo rows re-read by a neighbour tile hit that XCD's L2
+  int64_t first = blockIdx.x, stride = gridDim.x, last = ntiles;
+  if (gridDim.x % 8 == 0) {
+    const int64_t xcd = blockIdx.x % 8, nbx = gridDim.x / 8;
+    first = xcd * ntiles / 8 + blockIdx.x / 8;
+    last = (xcd + 1) * ntiles / 8;
+    stride = nbx;
+  }
+  int64_t b = first;
+  if (b < last) load_tile(b);
+  for (; b < last; b += stride) {
+    int64_t pl, i0, j0;
+    tile_of(b, pl, i0, j0);
+    T* dst = out + pl * n1 * n2;
+    auto store = [&](int i, int c, const Q4<T>& o) {  // tile row i, tile col c (multiple of 4)
+      const int64_t gi = i0 + i, gc = j0 + c;
+      if (gi >= n1) return;
+      if (vec && gc + 4 <= n2) {
+        stq(dst + gi * n2 + gc, o);
+      } else {
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
-#pragma unroll
-    for (int j = RB + KT - 2; j >= 0; --j) {
-      const Q4<T> v = ldq(buf + (i + j) * pitch + c);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int t = r + KT - 1 - j;
-        if (t >= 0 && t < KT) {
-#pragma unroll
-          for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
-        }
+        for (int m = 0; m < 4; ++m)
+          if (gc + m < n2) dst[gi * n2 + gc + m] = o.v[m];
       }
+    };
+    __syncthreads();  // the previous tile's passes are done with tin / mid
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = l * 256 + tid;
+      if (e < NR * GC) stq(tin + (e / GC) * WC + 4 * (e - (e / GC) * GC), q[l]);
     }
-  };
-  auto store = [&](int i, int c, const Q4<T>& o) {  // tile row i, tile col c (multiple of 4)
-    const int64_t gi = i0 + i, gc = j0 + c;
-    if (gi >= n1) return;
-    if (vec && gc + 4 <= n2) {
-      stq(dst + gi * n2 + gc, o);
+    __syncthreads();
+    if (b + stride < last) load_tile(b + stride);
+    if (VFIRST) {
+      // mid[i][c] (i < TY, all WC columns) = vertical pass: 32 lanes per block of RB rows
+      constexpr int RB = TY / 8;
+      for (int rb = half; rb < TY / RB; rb += 8) {
+        const int g = row_lane_group<GC>(l5);
+        Q4<T> acc[RB];
+        sep_vpass<T, RB, KT>(tin, WC, rb * RB, 4 * g, ha, acc);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) stq(mid + (rb * RB + r) * WC + 4 * g, acc[r]);
+      }
+      __syncthreads();
+      for (int i = 2 * half + lgrp; i < TY; i += 16) {
+        Q4<T> o;
+        hpass(mid + i * WC, 4 * lidx, o);
+        store(i, 4 * lidx, o);
+      }
     } else {
+      // mid[r][c] (all NR rows, TX columns) = horizontal pass
+      for (int r = 2 * half + lgrp; r < NR; r += 16) {
+        Q4<T> o;
+        hpass(tin + r * WC, 4 * lidx, o);
+        stq(mid + r * TX + 4 * lidx, o);
+      }
+      __syncthreads();
+      constexpr int RB = 2;
+      for (int rb = 2 * half + lgrp; rb < TY / RB; rb += 16) {
+        Q4<T> acc[RB];
+        sep_vpass<T, RB, KT>(mid, TX, rb * RB, 4 * lidx, ha, acc);
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-        if (gc + m < n2) dst[gi * n2 + gc + m] = o.v[m];
-    }
-  };
-  if (VFIRST) {
-    // mid[i][c] (i < TY, all WC columns) = vertical pass
-    for (int e = tid; e < (TY / RB) * GC; e += 256) {
-      const int rb = e / GC, g = e - (e / GC) * GC;
-      Q4<T> acc[RB];
-      vpass(tin, WC, rb * RB, 4 * g, acc);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) stq(mid + (rb * RB + r) * WC + 4 * g, acc[r]);
-    }
-    __syncthreads();
-    for (int e = tid; e < TY * (TX / 4); e += 256) {
-      const int i = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
-      Q4<T> o;
-      hpass(mid + i * WC, 4 * g, o);
-      store(i, 4 * g, o);
-    }
-  } else {
-    // mid[r][c] (all NR rows, TX columns) = horizontal pass
-    for (int e = tid; e < NR * (TX / 4); e += 256) {
-      const int r = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
-      Q4<T> o;
-      hpass(tin + r * WC, 4 * g, o);
-      stq(mid + r * TX + 4 * g, o);
-    }
-    __syncthreads();
-    for (int e = tid; e < (TY / RB) * (TX / 4); e += 256) {
-      const int rb = e / (TX / 4), g = e - (e / (TX / 4)) * (TX / 4);
-      Q4<T> acc[RB];
-      vpass(mid, TX, rb * RB, 4 * g, acc);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) store(rb * RB + r, 4 * g, acc[r]);
+        for (int r = 0; r < RB; ++r) store(rb * RB + r, 4 * lidx, acc[r]);
+      }
     }
   }
 }
@@ -538,15 +599,32 @@ template <typename T, bool VFIRST>
 static void launch_sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
                          const void* hb, int kb, int offb, hipStream_t st) {
   using S = Sep2D<T>;
-  const unsigned g = (unsigned)(np * ((n1 + S::TY - 1) / S::TY) * ((n2 + S::TX - 1) / S::TX));
+  const int64_t nt = np * ((n1 + S::TY - 1) / S::TY) * ((n2 + S::TX - 1) / S::TX);
+  // persistent: ~4 blocks per CU, a multiple of 8 (XCDs) when the tiles allow
+  static int64_t cap = 0;
+  if (cap == 0) {  // PCS_SEP2D_BLOCKS: diagnostics override of the persistent grid
+    const char* e = getenv("PCS_SEP2D_BLOCKS");
+    cap = e ? atoll(e) : kSep2DBlocks;
+    if (cap < 8) cap = kSep2DBlocks;
+  }
+  const unsigned g = (unsigned)(nt >= cap ? cap : nt);
   auto args = [&](auto kern) {
     kern<<<g, 256, 0, st>>>((const T*)in, (T*)out, np, n1, n2, (const T*)ha, ka, offa, (const T*)hb, kb, offb);
   };
-  switch ((S::CH + offb - (S::KT - 1)) & 3) {
-    case 0: args(k_sep2d<T, 0, VFIRST>); break;
-    case 1: args(k_sep2d<T, 1, VFIRST>); break;
-    case 2: args(k_sep2d<T, 2, VFIRST>); break;
-    default: args(k_sep2d<T, 3, VFIRST>); break;
+  if (n2 % 4 == 0) {
+    switch ((S::CH + offb - (S::KT - 1)) & 3) {
+      case 0: args(k_sep2d<T, 0, VFIRST, true>); break;
+      case 1: args(k_sep2d<T, 1, VFIRST, true>); break;
+      case 2: args(k_sep2d<T, 2, VFIRST, true>); break;
+      default: args(k_sep2d<T, 3, VFIRST, true>); break;
+    }
+  } else {
+    switch ((S::CH + offb - (S::KT - 1)) & 3) {
+      case 0: args(k_sep2d<T, 0, VFIRST, false>); break;
+      case 1: args(k_sep2d<T, 1, VFIRST, false>); break;
+      case 2: args(k_sep2d<T, 2, VFIRST, false>); break;
+      default: args(k_sep2d<T, 3, VFIRST, false>); break;
+    }
   }
 }
 

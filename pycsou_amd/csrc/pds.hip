@@ -9,6 +9,7 @@
 // precomputed gradient buffer; K = Gradient(kind='forward'); H = lam*L1 / lam*L21 (pixel
 // groups); G = Null / NonNegativeOrthant / Segment.  The tile kernel is in pds_tile.hpp.
 #include "pds_march.hpp"
+#include "pds_pt.hpp"
 
 namespace pcs {
 
@@ -221,9 +222,82 @@ static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
   return a->hkind == PCS_H_L21 ? launch_march<H, PCS_H_L21>(a, st) : launch_march<H, PCS_H_L1>(a, st);
 }
 
+// ---- fp32 pointwise grad F (NULL / DENOISE / GRADBUF): the row-marching kernel of pds_pt.hpp
+static int pt_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_pt<PCS_F_DENOISE, PCS_H_L21>, 256, 0) !=
+            hipSuccess ||
+        nb < 1)
+      nb = 4;
+    (void)hipGetLastError();
+    slots = cus * nb;
+  }
+  return slots;
+}
+
+// tasks = 64-column strips x row segments of >= 4 steps, about one wave of resident blocks
+static bool pt_plan(const pcs_pds2d_args* a, MarchPlan* p) {
+  constexpr int TS = PtGeom::TS;
+  p->tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
+  if (p->tiles_x < 2) return false;
+  const int64_t steps = (a->rows + TS - 1) / TS;
+  int64_t nseg = pt_slots() / p->tiles_x;
+  const int64_t max_seg = (steps + 3) / 4;
+  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
+  const int64_t steps_per = (steps + nseg - 1) / nseg;
+  p->seg_len = (int)(steps_per * TS);
+  nseg = (a->rows + p->seg_len - 1) / p->seg_len;
+  p->ntasks = (int)(p->tiles_x * nseg);
+  return true;
+}
+
+static bool use_pt(const pcs_pds2d_args* a) {
+  static int disabled = -1;  // PCS_NO_MARCH=1: diagnostics, force the tile kernel
+  if (disabled < 0) disabled = getenv("PCS_NO_MARCH") != nullptr;
+  if (disabled) return false;
+  if (a->dtype != PCS_F32 || !make_slab(a).vec) return false;
+  if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF) return false;
+  if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return false;
+  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
+                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
+  MarchPlan p;
+  return pt_plan(a, &p);
+}
+
+template <int FK, int HK>
+static int launch_pt(const pcs_pds2d_args* a, hipStream_t st) {
+  MarchPlan p;
+  if (!pt_plan(a, &p)) return PCS_EINVAL;
+  const Slab s64 = make_slab(a);
+  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
+  const Params<float> P = make_params<float>(a);
+  const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
+  k_pds2d_pt<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z,
+                                                         (float*)a->zn, g, s, P, a->gkind, a->partials,
+                                                         (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles_x, p.seg_len,
+                                                         p.ntasks);
+  return launch_status();
+}
+
+template <int FK>
+static int launch_pt(const pcs_pds2d_args* a, hipStream_t st) {
+  return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, st) : launch_pt<FK, PCS_H_L1>(a, st);
+}
+
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, st) : launch_march<7>(a, st);
+  if (use_pt(a)) {
+    if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, st);
+    if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, st);
+    return launch_pt<PCS_F_NULL>(a, st);
+  }
   switch (a->fkind) {
     case PCS_F_NULL: return launch_pds2d<T, PCS_F_NULL, 0>(a, st);
     case PCS_F_DENOISE: return launch_pds2d<T, PCS_F_DENOISE, 0>(a, st);
@@ -260,6 +334,11 @@ int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
     MarchPlan p;
     if (tier_for(a->half) == 3) march_plan<3>(a, &p);
     else march_plan<7>(a, &p);
+    return (int64_t)p.ntasks;
+  }
+  if (use_pt(a)) {
+    MarchPlan p;
+    pt_plan(a, &p);
     return (int64_t)p.ntasks;
   }
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;

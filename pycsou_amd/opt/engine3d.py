@@ -202,13 +202,15 @@ class PDS3DEngine:
                                     int(axis), L.ptr(taps), int(k), int(off), st), 'pcs_conv1d')
 
     def _sep_planes(self, src, dst, np_, ops, flipped, st):
-        """Both in-plane passes of `ops` (axis 1 and axis 2, application order) in one launch."""
+        """Both in-plane passes of `ops` (one along axis 1, one along axis 2) in one launch.  The
+        two convolutions commute; the axis-2 pass runs first (the faster kernel order,
+        tools/sep2d_probe.py), which changes only the rounding order of the sums."""
         (a0, h0, hf0, k0, o0), (a1, h1, hf1, k1, o1) = ops
         first, second = (h0, k0, o0) if not flipped else (hf0, k0, k0 - 1 - o0), \
                         (h1, k1, o1) if not flipped else (hf1, k1, k1 - 1 - o1)
         (ha, ka, oa), (hb, kb, ob) = (first, second) if a0 == 1 else (second, first)
         L.check(self.lib.pcs_conv2d_sep_planes(self.base_args.dtype, src, dst, np_, self.n1, self.n2, L.ptr(ha), ka, oa,
-                                               L.ptr(hb), kb, ob, int(a0 == 1), st), 'pcs_conv2d_sep_planes')
+                                               L.ptr(hb), kb, ob, 0, st), 'pcs_conv2d_sep_planes')
 
     def _gradient_fused0(self, p, st):
         nsub = self.rows + 2 * self.hx

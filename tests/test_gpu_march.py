@@ -1,7 +1,8 @@
-"""The row-marching fused step (pds_march.hpp: fp32, separable PSF of half-width <= 7, n1 >= 128,
-n1 % 4 == 0) against the fp64 oracle, on shapes that exercise its edges: partial last strip,
-several row segments with a short last one, both tap tiers (3, 7) and PSFs narrower than their
-tier, L1 / L21, every prox_G kind, non-unit gradient steps.
+"""The row-marching fused steps against the fp64 oracle: pds_march.hpp (fp32, separable PSF of
+half-width <= 7) and pds_pt.hpp (fp32 denoising, grad F = x - y, and non-separable PSFs through
+the gradient buffer), n1 >= 128, n1 % 4 == 0, on shapes that exercise their edges: partial
+last strip, several row segments with a short last one, both tap tiers (3, 7) and PSFs narrower
+than their tier, L1 / L21, every prox_G kind, non-unit gradient steps.
 
 Tolerance: relative L2 of x and z <= 5e-5 after 12 iterations (fp32 against fp64, as the golden
 fp32 cases), diagnostics to 2e-2 relative, iteration counts exact.
@@ -23,10 +24,17 @@ def _problem(shape, psf_len, hname, gname, steps, seed):
     n0, n1 = shape
     N = n0 * n1
     xs = OR.phantom(shape, seed=seed)
-    r = np.arange(psf_len) - psf_len // 2
-    t0 = np.exp(-0.5 * (r / 1.7) ** 2)
-    t1 = np.exp(-0.5 * (r / 2.3) ** 2)
-    psf = np.outer(t0 / t0.sum(), t1 / t1.sum())
+    if psf_len == 0:  # denoising: no operator in F
+        psf = None
+    elif psf_len < 0:  # non-separable (rank 2) -|psf_len| x -|psf_len| PSF: gradient-buffer path
+        q = -psf_len
+        psf = rng.uniform(0.0, 1.0, (q, q))
+        psf /= psf.sum()
+    else:
+        r = np.arange(psf_len) - psf_len // 2
+        t0 = np.exp(-0.5 * (r / 1.7) ** 2)
+        t1 = np.exp(-0.5 * (r / 2.3) ** 2)
+        psf = np.outer(t0 / t0.sum(), t1 / t1.sum())
     return dict(shape=shape, N=N, psf=psf, y=xs.ravel() + 0.05 * rng.standard_normal(N), hname=hname, gname=gname,
                 steps=steps, lam=0.05)
 
@@ -34,8 +42,12 @@ def _problem(shape, psf_len, hname, gname, steps, seed):
 def _oracle(p):
     from oracle import pylops1 as P
     shape, N, psf, y = p['shape'], p['N'], p['psf'], p['y']
-    off = tuple(P.pycsou_offset(n) for n in psf.shape)
-    C = P.Convolve2D(N, psf, shape, offset=off)
+    if psf is None:
+        grad = lambda v: (2 * (v + (-y))) * 0.5  # noqa: E731
+    else:
+        off = tuple(P.pycsou_offset(n) for n in psf.shape)
+        C = P.Convolve2D(N, psf, shape, offset=off)
+        grad = lambda v: C.rmatvec((2 * (C.matvec(v) + (-y))) * 0.5)  # noqa: E731
     K = P.Gradient(shape, sampling=p['steps'], edge=True, kind='forward')
     if p['hname'] == 'l21':
         hprox = OR.postcomp(lambda v, t: OR.prox_l21_pixel(v, t, 2), p['lam'])
@@ -46,7 +58,7 @@ def _oracle(p):
     beta = 1.0
     lip = np.sqrt(sum(4.0 / s ** 2 for s in p['steps']))
     tau, sigma = OR.pds_step_sizes(beta, lip)[:2]
-    x, z, d = OR.pds(lambda v: C.rmatvec((2 * (C.matvec(v) + (-y))) * 0.5), gprox, K.matvec, K.rmatvec,
+    x, z, d = OR.pds(grad, gprox, K.matvec, K.rmatvec,
                      lambda w, s: OR.fenchel_prox(hprox, w, s), tau, sigma, 0.9, np.zeros(N), np.zeros(2 * N),
                      max_iter=NITER - 1, min_iter=NITER - 1, accuracy_threshold=0.0)
     return x, z, d, lip
@@ -59,13 +71,16 @@ def _fused(p, lip):
     from pycsou_amd.linop.diff import Gradient
     from pycsou_amd.opt.proxalgs import PDS
     shape, N = p['shape'], p['N']
-    C = Convolve2D(N, p['psf'], shape)
-    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=p['y'].astype(np.float32))
+    if p['psf'] is not None:
+        C = Convolve2D(N, p['psf'], shape)
+        C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+        F = F * C
     K = Gradient(shape, step=p['steps'], kind='forward')
     K.lipschitz_cst = K.diff_lipschitz_cst = lip
     H = p['lam'] * (L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)) if p['hname'] == 'l21' else L1Norm(dim=2 * N))
     G = {'nonneg': NonNegativeOrthant(N), 'segment': Segment(N, 0.0, 1.0)}.get(p['gname'], None)
-    pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=p['y'].astype(np.float32)) * C, G=G, H=H, K=K,
+    pds = PDS(dim=N, F=F, G=G, H=H, K=K,
               x0=np.zeros(N, np.float32), z0=np.zeros(2 * N, np.float32), max_iter=NITER - 1, min_iter=NITER - 1,
               accuracy_threshold=0.0, verbose=None, engine='fused')
     est, _, diag = pds.iterate()
@@ -81,6 +96,10 @@ CASES = [
     ((190, 256), 5, 'l1', '', (2.0, 0.5)),          # psf half 2 in tier 3, non-unit steps
     ((1000, 128), 15, 'l1', 'segment', (0.5, 1.0)),  # tall: many row segments, short last one
     ((1000, 4096), 15, 'l21', 'nonneg', (1.0, 1.0)),  # C3 width: 6-step tasks, 3-step last segment
+    # pds_pt.hpp
+    ((300, 200), 0, 'l21', '', (1.0, 1.0)),            # denoising, partial last strip
+    ((1030, 2048), 0, 'l1', 'segment', (2.0, 0.5)),    # denoising, C2 width, short last segment
+    ((261, 132), -5, 'l21', 'nonneg', (1.0, 1.0)),     # non-separable 5x5 PSF (gradient buffer)
 ]
 
 

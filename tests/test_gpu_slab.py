@@ -106,6 +106,34 @@ def test_c3_slabs_bitwise(world):
     assert np.allclose(res[0][3][1:], h1[1:], rtol=1e-5)
 
 
+@pytest.mark.parametrize('world', [3, 5])
+def test_denoise_slabs_bitwise(world):
+    """fp32 TV denoising 700 x 256 (the pointwise-F march kernel, pds_pt.hpp) split into uneven
+    row slabs: bitwise equal to the single-GPU engine, 20 fixed iterations."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.opt.proxalgs import PDS
+    from pycsou_amd.parallel import SlabPDS2D, run_local
+    n0, n1 = 700, 256
+    N = n0 * n1
+    y = torch.as_tensor(np.random.default_rng(2).uniform(0, 1, N).astype(np.float32)).cuda()
+    K = Gradient((n0, n1), kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = np.sqrt(8.0)
+    pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y), H=0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)),
+              K=K, x0=torch.zeros(N, device='cuda'), z0=torch.zeros(2 * N, device='cuda'), verbose=None)
+    spec = pds._fused_spec()
+    eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    n, x1, z1, h1 = eng.run(19, 19, 0.0)
+    slabs = [SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, r, world)
+             for r in range(world)]
+    res = run_local(slabs, 19, 19, 0.0)
+    assert all(r[0] == n == 20 for r in res)
+    assert torch.equal(torch.cat([r[1] for r in res]), x1)
+    assert np.allclose(res[0][3][1:], h1[1:], rtol=1e-5)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
