@@ -177,10 +177,68 @@ int pcs_pds2d_halo_x(int half);
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
 int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a);
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
+/* pcs_pds2d_step restricted to the slab's own rows [ra0, rb0) u [ra1, rb1)
+ * (0 <= ra0 <= rb0 <= ra1 <= rb1 <= rows): writes x', z' on those rows and one partials row per
+ * block (pcs_pds2d_nblocks_bands of them); hist must be NULL.  Same arithmetic per pixel as the
+ * whole-slab step, so any split of the rows into launches gives bitwise the same x', z'.  The
+ * multi-GPU loop runs the boundary bands and the interior band as separate launches so that the
+ * halo exchange overlaps the interior.  Row-marching kernels only (fp32, L1/L21; F separable
+ * conv of half width <= 7, or pointwise): PCS_EUNSUPPORTED otherwise. */
+int64_t pcs_pds2d_nblocks_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1);
+int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1,
+                         hipStream_t stream);
 /* n iterations of pcs_pds2d_step launched back to back, ping-ponging (x, z) <-> (xn, zn)
  * (even n leaves the iterate in x, z); requires hist/ctrl/ws (in-kernel loop control).  The
  * host-side form of GenericIterativeAlgorithm.iterate's loop (pycsou/core/solver.py:55-76). */
 int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t stream);
+
+/* ---------------------------------------------------------------- multi-GPU row slabs
+ * Native per-rank loop of the row-slab 2-D PDS (one process per GPU, RCCL over xGMI):
+ * GenericIterativeAlgorithm.iterate (pycsou/core/solver.py:55-76) around
+ * PrimalDualSplitting.update_iterand / update_diagnostics (pycsou/opt/proxalgs.py:343-394) for an
+ * image split into contiguous row slabs.  Per iteration: the fused slab step, the four norm sums
+ * all-gathered (4 doubles per rank, added in rank order, so every rank takes the same stop
+ * decision) and the boundary rows of x', z' exchanged with the two neighbour ranks.
+ * RCCL is bound at run time (dlopen librccl.so.1); pcs_comm_available() says whether it was. */
+int pcs_comm_available(void);
+int pcs_comm_id_bytes(void); /* size of the opaque unique id (ncclUniqueId) */
+int pcs_comm_unique_id(void* id);                               /* rank 0; broadcast id to the others */
+int pcs_comm_init(const void* id, int world, int rank, void** comm); /* collective over the ranks */
+int pcs_comm_destroy(void* comm);
+
+/* Halo buffers written by one parity of the ping-pong (up to 4 arrays, e.g. x', z0', z1'):
+ * send_lo[k] (own first rows) goes to rank-1's recv_hi[k]; send_hi[k] (own last rows) to
+ * rank+1's recv_lo[k]; bytes[k] bytes each.  Pointers toward a missing neighbour may be NULL. */
+typedef struct {
+  int nbuf;
+  int pad;
+  void* send_lo[4];
+  void* recv_lo[4];
+  void* send_hi[4];
+  void* recv_hi[4];
+  int64_t bytes[4];
+} pcs_halo_set;
+
+typedef struct {
+  int world, rank;
+  pcs_pds2d_args step[2]; /* parity p: x = X[p] -> xn = X[1-p] (hist/ws ignored, partials owned by the plan) */
+  pcs_halo_set halo[2];   /* halo[p]: the buffers step[p] writes (X[1-p], Z[1-p]) */
+  void* ctrl;             /* loop control block (pcs_ctrl_init2), identical on every rank */
+  double* hist;
+  int64_t band;           /* boundary band rows (>= the x halo depth) for the overlapped schedule */
+  int overlap;            /* 1: boundary bands, then the halo exchange on a side stream while the
+                             interior band runs (row-marching kernels only; else the serial schedule) */
+  int pad2;
+} pcs_slab2d_desc;
+
+/* comm may be NULL when world == 1.  The plan owns its partials/sums buffers, a side stream and
+ * events (allocated here, not in pcs_slab2d_run). */
+int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan);
+int pcs_slab2d_overlapped(const void* plan);
+/* n iterations starting at parity p0 (no host synchronisation; the stop flag in ctrl makes the
+ * iterations after the reference loop's exit return at once). */
+int pcs_slab2d_run(void* plan, int64_t n, int p0, hipStream_t stream);
+int pcs_slab2d_destroy(void* plan);
 
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics for 3-D volumes
  * (pycsou/opt/proxalgs.py:343-394), K = Gradient(kind='forward') in 3-D

@@ -49,6 +49,18 @@ class Pds3Args(ctypes.Structure):
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
 
 
+class HaloSet(ctypes.Structure):
+    """Mirror of pcs_halo_set."""
+    _fields_ = [('nbuf', _c_int), ('pad', _c_int), ('send_lo', _vp * 4), ('recv_lo', _vp * 4),
+                ('send_hi', _vp * 4), ('recv_hi', _vp * 4), ('bytes', _c_i64 * 4)]
+
+
+class Slab2DDesc(ctypes.Structure):
+    """Mirror of pcs_slab2d_desc."""
+    _fields_ = [('world', _c_int), ('rank', _c_int), ('step', PdsArgs * 2), ('halo', HaloSet * 2),
+                ('ctrl', _vp), ('hist', _vp), ('band', _c_i64), ('overlap', _c_int), ('pad2', _c_int)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     'pcs_abi_version': (_c_int, []),
@@ -83,6 +95,17 @@ _SIGS = {
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
+    'pcs_pds2d_nblocks_bands': (_c_i64, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64]),
+    'pcs_pds2d_step_bands': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64, _vp]),
+    'pcs_comm_available': (_c_int, []),
+    'pcs_comm_id_bytes': (_c_int, []),
+    'pcs_comm_unique_id': (_c_int, [_vp]),
+    'pcs_comm_init': (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(_vp)]),
+    'pcs_comm_destroy': (_c_int, [_vp]),
+    'pcs_slab2d_create': (_c_int, [ctypes.POINTER(Slab2DDesc), _vp, ctypes.POINTER(_vp)]),
+    'pcs_slab2d_overlapped': (_c_int, [_vp]),
+    'pcs_slab2d_run': (_c_int, [_vp, _c_i64, _c_int, _vp]),
+    'pcs_slab2d_destroy': (_c_int, [_vp]),
     'pcs_pds3d_nblocks': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_ws_bytes': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_step': (_c_int, [ctypes.POINTER(Pds3Args), _vp]),

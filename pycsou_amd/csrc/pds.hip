@@ -147,9 +147,35 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
 constexpr int kMarchNT = 256;
 
 struct MarchPlan {
-  int tiles_x;                   // 64-column strips
-  int seg_len, ntasks;           // rows per task, tasks (strips x row segments)
+  int tiles_x;  // 64-column strips
+  Bands bd;     // row segments of the launch's bands
+  int ntasks;   // strips x segments
 };
+
+// own-row bands [ra0, rb0) and [ra1, rb1) of a launch (0 <= ra0 <= rb0 <= ra1 <= rb1 <= rows)
+struct RowBands {
+  int64_t ra0, rb0, ra1, rb1;
+};
+static RowBands full_bands(const pcs_pds2d_args* a) { return RowBands{0, a->rows, a->rows, a->rows}; }
+
+// Segments of TS-row steps over the bands: about `slots / tiles_x` segments in all (one wave of
+// resident workgroups), at least one per non-empty band, at most one per `min_steps` steps.
+static void plan_bands(RowBands rb, int TS, int tiles_x, int slots, int min_steps, MarchPlan* p) {
+  if (rb.rb0 == rb.ra0) rb = RowBands{rb.ra1, rb.rb1, rb.rb1, rb.rb1};
+  const int64_t L0 = rb.rb0 - rb.ra0, L1 = rb.rb1 - rb.ra1;
+  const int64_t steps = (L0 + TS - 1) / TS + (L1 + TS - 1) / TS;
+  const int64_t bands = (L0 > 0) + (L1 > 0);
+  int64_t nseg = slots / tiles_x;
+  const int64_t max_seg = (steps + min_steps - 1) / min_steps;
+  nseg = nseg > max_seg ? max_seg : nseg;
+  nseg = nseg < bands ? bands : nseg;
+  nseg = nseg < 1 ? 1 : nseg;
+  const int64_t seg_len = ((steps + nseg - 1) / nseg) * TS;
+  const int64_t n0 = (L0 + seg_len - 1) / seg_len, n1 = (L1 + seg_len - 1) / seg_len;
+  p->tiles_x = tiles_x;
+  p->bd = Bands{(int)seg_len, (int)n0, (int)rb.ra0, (int)rb.rb0, (int)rb.ra1, (int)rb.rb1};
+  p->ntasks = (int)(tiles_x * (n0 + n1));
+}
 
 // resident workgroups of the march kernel on the whole device (queried once)
 template <int H>
@@ -173,18 +199,11 @@ static int march_slots() {
 // One march task = one 64-column strip x one row segment; as many segments as fill the
 // device in one wave of resident workgroups.  False for narrow images (the tile kernel).
 template <int H>
-static bool march_plan(const pcs_pds2d_args* a, MarchPlan* p) {
+static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   using M = March<H>;
-  constexpr int TS = M::TS;
-  p->tiles_x = (int)((a->n1 + M::TW - 1) / M::TW);
-  if (p->tiles_x < 2) return false;
-  const int64_t steps = (a->rows + TS - 1) / TS;
-  int64_t nseg = march_slots<H>() / p->tiles_x;
-  nseg = nseg < 1 ? 1 : (nseg > steps ? steps : nseg);
-  const int64_t steps_per = (steps + nseg - 1) / nseg;
-  p->seg_len = (int)(steps_per * TS);
-  nseg = (a->rows + p->seg_len - 1) / p->seg_len;
-  p->ntasks = (int)(p->tiles_x * nseg);
+  const int tiles_x = (int)((a->n1 + M::TW - 1) / M::TW);
+  if (tiles_x < 2) return false;
+  plan_bands(rb, M::TS, tiles_x, march_slots<H>(), 1, p);
   return true;
 }
 
@@ -200,26 +219,27 @@ static bool use_march(const pcs_pds2d_args* a) {
   // 32-bit indexing and buffer views of at most 2^30 bytes (pds_march.hpp kOOB)
   if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
   MarchPlan p;
-  return t == 3 ? march_plan<3>(a, &p) : march_plan<7>(a, &p);
+  return t == 3 ? march_plan<3>(a, full_bands(a), &p) : march_plan<7>(a, full_bands(a), &p);
 }
 
 template <int H, int HK>
-static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
+static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   MarchPlan p;
-  if (!march_plan<H>(a, &p)) return PCS_EINVAL;
+  if (!march_plan<H>(a, rb, &p)) return PCS_EINVAL;
+  if (p.ntasks == 0) return PCS_OK;
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
   k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
-      a->ws, p.tiles_x, p.seg_len, p.ntasks);
+      a->ws, p.tiles_x, p.bd, p.ntasks);
   return launch_status();
 }
 
 template <int H>
-static int launch_march(const pcs_pds2d_args* a, hipStream_t st) {
-  return a->hkind == PCS_H_L21 ? launch_march<H, PCS_H_L21>(a, st) : launch_march<H, PCS_H_L1>(a, st);
+static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  return a->hkind == PCS_H_L21 ? launch_march<H, PCS_H_L21>(a, rb, st) : launch_march<H, PCS_H_L1>(a, rb, st);
 }
 
 // ---- fp32 pointwise grad F (NULL / DENOISE / GRADBUF): the row-marching kernel of pds_pt.hpp
@@ -241,18 +261,10 @@ static int pt_slots() {
 }
 
 // tasks = 64-column strips x row segments of >= 4 steps, about one wave of resident blocks
-static bool pt_plan(const pcs_pds2d_args* a, MarchPlan* p) {
-  constexpr int TS = PtGeom::TS;
-  p->tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
-  if (p->tiles_x < 2) return false;
-  const int64_t steps = (a->rows + TS - 1) / TS;
-  int64_t nseg = pt_slots() / p->tiles_x;
-  const int64_t max_seg = (steps + 3) / 4;
-  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
-  const int64_t steps_per = (steps + nseg - 1) / nseg;
-  p->seg_len = (int)(steps_per * TS);
-  nseg = (a->rows + p->seg_len - 1) / p->seg_len;
-  p->ntasks = (int)(p->tiles_x * nseg);
+static bool pt_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
+  const int tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
+  if (tiles_x < 2) return false;
+  plan_bands(rb, PtGeom::TS, tiles_x, pt_slots(), 4, p);
   return true;
 }
 
@@ -267,37 +279,41 @@ static bool use_pt(const pcs_pds2d_args* a) {
                                              : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
   if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
   MarchPlan p;
-  return pt_plan(a, &p);
+  return pt_plan(a, full_bands(a), &p);
 }
 
 template <int FK, int HK>
-static int launch_pt(const pcs_pds2d_args* a, hipStream_t st) {
+static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   MarchPlan p;
-  if (!pt_plan(a, &p)) return PCS_EINVAL;
+  if (!pt_plan(a, rb, &p)) return PCS_EINVAL;
+  if (p.ntasks == 0) return PCS_OK;
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
   const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
   k_pds2d_pt<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z,
                                                          (float*)a->zn, g, s, P, a->gkind, a->partials,
-                                                         (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles_x, p.seg_len,
+                                                         (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles_x, p.bd,
                                                          p.ntasks);
   return launch_status();
 }
 
 template <int FK>
-static int launch_pt(const pcs_pds2d_args* a, hipStream_t st) {
-  return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, st) : launch_pt<FK, PCS_H_L1>(a, st);
+static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, rb, st) : launch_pt<FK, PCS_H_L1>(a, rb, st);
+}
+
+// the row-marching families (march, pt) take row bands; the tile kernel runs whole slabs only
+static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, rb, st) : launch_march<7>(a, rb, st);
+  if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, rb, st);
+  if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, rb, st);
+  return launch_pt<PCS_F_NULL>(a, rb, st);
 }
 
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
-  if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, st) : launch_march<7>(a, st);
-  if (use_pt(a)) {
-    if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, st);
-    if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, st);
-    return launch_pt<PCS_F_NULL>(a, st);
-  }
+  if (use_march(a) || use_pt(a)) return pds2d_bands(a, full_bands(a), st);
   switch (a->fkind) {
     case PCS_F_NULL: return launch_pds2d<T, PCS_F_NULL, 0>(a, st);
     case PCS_F_DENOISE: return launch_pds2d<T, PCS_F_DENOISE, 0>(a, st);
@@ -312,6 +328,20 @@ static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
       }
     default: return PCS_EINVAL;
   }
+}
+
+static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb) {
+  MarchPlan p;
+  if (use_march(a)) {
+    if (tier_for(a->half) == 3) march_plan<3>(a, rb, &p);
+    else march_plan<7>(a, rb, &p);
+    return (int64_t)p.ntasks;
+  }
+  if (use_pt(a)) {
+    pt_plan(a, rb, &p);
+    return (int64_t)p.ntasks;
+  }
+  return -1;
 }
 
 static int needed_halo_x(int fkind, int half) {
@@ -330,17 +360,7 @@ int pcs_pds2d_halo_x(int half) { return 1 + 2 * tier_for(half < 0 ? 0 : half); }
 
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
   if (!a || a->rows < 1 || a->n1 < 1) return -1;
-  if (use_march(a)) {
-    MarchPlan p;
-    if (tier_for(a->half) == 3) march_plan<3>(a, &p);
-    else march_plan<7>(a, &p);
-    return (int64_t)p.ntasks;
-  }
-  if (use_pt(a)) {
-    MarchPlan p;
-    pt_plan(a, &p);
-    return (int64_t)p.ntasks;
-  }
+  if (use_march(a) || use_pt(a)) return bands_nblocks(a, full_bands(a));
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);
 }
@@ -350,7 +370,7 @@ int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a) {
   return nb < 0 ? -1 : red_ws_bytes(nb);
 }
 
-int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
+static int check_args(const pcs_pds2d_args* a) {
   if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
   if (a->hist && (!a->ws || !a->ctrl || !aligned16(a->ws) || !aligned16(a->partials))) return PCS_EINVAL;
   if (a->n0 < 1 || a->n1 < 1 || a->rows < 1 || a->row0 < 0 || a->row0 + a->rows > a->n0) return PCS_EINVAL;
@@ -367,6 +387,30 @@ int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
                 ((a->fkind == PCS_F_SEPCONV) && a->halo_y < tier_for(a->half) + 1) ||
                 ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_GRADBUF) && a->halo_y < 1)))
     return PCS_EINVAL;
+  return PCS_OK;
+}
+
+static bool bands_ok(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1) {
+  return 0 <= ra0 && ra0 <= rb0 && rb0 <= ra1 && ra1 <= rb1 && rb1 <= a->rows;
+}
+
+int64_t pcs_pds2d_nblocks_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1) {
+  if (check_args(a) != PCS_OK || !bands_ok(a, ra0, rb0, ra1, rb1)) return -1;
+  return bands_nblocks(a, RowBands{ra0, rb0, ra1, rb1});
+}
+
+int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1,
+                         hipStream_t st) {
+  const int rc = check_args(a);
+  if (rc != PCS_OK) return rc;
+  if (a->hist || !bands_ok(a, ra0, rb0, ra1, rb1)) return PCS_EINVAL;
+  if (!(use_march(a) || use_pt(a))) return PCS_EUNSUPPORTED;
+  return pds2d_bands(a, RowBands{ra0, rb0, ra1, rb1}, st);
+}
+
+int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
+  const int rc = check_args(a);
+  if (rc != PCS_OK) return rc;
   if (a->dtype == PCS_F32) return pds2d<float>(a, st);
   if (a->dtype == PCS_F64) return pds2d<double>(a, st);
   return PCS_EINVAL;

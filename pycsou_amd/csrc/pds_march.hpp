@@ -86,6 +86,23 @@ __device__ __forceinline__ unsigned long long pcs_stamp() {
 // global data another wave of the launch wrote.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Own-row bands of one launch: segments [ra0, rb0) first (nseg0 of them), then [ra1, rb1).
+// The whole slab is {seg_len, nseg, 0, rows, rows, rows}; the multi-GPU loop launches the
+// two boundary bands (the rows its neighbours' halos need) apart from the interior band so
+// that the halo exchange overlaps the interior.
+struct Bands {
+  int seg_len, nseg0, ra0, rb0, ra1, rb1;
+};
+__device__ __forceinline__ void band_rows(const Bands& bd, int seg, int& s0, int& s1) {
+  if (seg < bd.nseg0) {
+    s0 = bd.ra0 + seg * bd.seg_len;
+    s1 = min(s0 + bd.seg_len, bd.rb0);
+  } else {
+    s0 = bd.ra1 + (seg - bd.nseg0) * bd.seg_len;
+    s1 = min(s0 + bd.seg_len, bd.rb1);
+  }
+}
+
 // 32-bit slab geometry (the host checks (rows + 2 halo) * n1 < 2^31 for this kernel)
 struct Slab32 {
   int n0, n1, row0, rows, hx, hy, hz, vec;
@@ -592,7 +609,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
     const T* __restrict__ y, const T* __restrict__ taps0, const T* __restrict__ taps1, int half, Slab32 s,
     Params<T> P, int gk, double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws, int tiles_x,
-    int seg_len, int ntasks) {
+    Bands bd, int ntasks) {
   using M = March<H>;
   __shared__ __attribute__((aligned(16))) T sm[M::SZ];
   __shared__ double red[4 * (NT / 64)];
@@ -606,8 +623,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
-  const int s0 = seg * seg_len;
-  const int s1 = min(s0 + seg_len, s.rows);
+  int s0, s1;
+  band_rows(bd, seg, s0, s1);
   const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
                                                    const float* __restrict__ z, float* __restrict__ zn,
                                                    const float* __restrict__ gsrc, Slab32 s, Params<float> P, int gk,
                                                    double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
-                                                   int tiles_x, int seg_len, int ntasks) {
+                                                   int tiles_x, Bands bd, int ntasks) {
   __shared__ __attribute__((aligned(16))) float sm[PtGeom::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
@@ -236,8 +236,8 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
-  const int s0 = seg * seg_len;
-  const int s1 = min(s0 + seg_len, s.rows);
+  int s0, s1;
+  band_rows(bd, seg, s0, s1);
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   pt_task<FK, HK>(x, xn, z, zn, gsrc, s, P, gk, s0, s1, strip * PtGeom::TW, sm, part);
   block_sum<4>(part, red);

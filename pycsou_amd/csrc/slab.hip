@@ -1,0 +1,273 @@
+// Native multi-GPU loop of the row-slab 2-D PDS (one process per GPU, RCCL over xGMI).
+//
+// Replaces, for an image split into row slabs across ranks, the host loop of
+//   GenericIterativeAlgorithm.iterate     pycsou/core/solver.py:55-76
+// around PrimalDualSplitting.update_iterand / update_diagnostics (pycsou/opt/proxalgs.py:343-394):
+// every iteration runs the fused step on this rank's own rows, sums the four norm partials
+// across ranks (RCCL all-gather of 4 doubles per rank, added in rank order on every rank, so
+// all ranks take the same stop decision) and exchanges the boundary rows of x' and z' with
+// the two neighbour ranks (grouped RCCL send/recv).
+//
+// Overlap mode (row-marching kernels): the boundary bands (the rows the neighbours' halos
+// need, and the rows that read our halos) are computed first, then the halo exchange runs on
+// a side stream while the interior band is computed on the main stream; the norms all-gather
+// and the loop control run on the side stream behind the next iteration's boundary launch.
+// That makes iteration i+1 start before iteration i's stop decision is known: it writes only
+// the other ping-pong buffers, and iteration i+2 is ordered after that decision (its boundary
+// launch waits for the halo exchange that follows it on the side stream), so a stop after
+// iteration i leaves iteration i's iterate untouched and every later launch returns at once.
+//
+// RCCL is bound at run time (dlopen of librccl.so.1: the copy the process already loaded,
+// e.g. PyTorch's, or the ROCm one), so the library loads and the single-GPU paths run
+// without it.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+
+#include "common.hpp"
+
+namespace pcs {
+
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  bool ok = false;
+};
+
+static const Rccl& rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+      r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+      r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+      r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+      r.send = (decltype(r.send))dlsym(h, "ncclSend");
+      r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
+      r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+      r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+      r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.send && r.recv &&
+             r.group_start && r.group_end;
+    }
+  }
+  return r;
+}
+
+struct Slab2DPlan {
+  pcs_slab2d_desc d;
+  ncclComm_t comm;
+  hipStream_t side;
+  hipEvent_t ev_fork, ev_b, ev_halo, ev_sum, ev_join;
+  double* partials;   // [nB + nI] (overlap) or [nfull] partial rows of 4
+  double* sums;       // [2][4]
+  double* gathered;   // [2][4 world]
+  int64_t nfull, nB, nI;
+  bool overlap;
+};
+
+static int halo_exchange(const Slab2DPlan& P, const pcs_halo_set& h, hipStream_t st) {
+  const Rccl& R = rccl();
+  const int lo = P.d.rank - 1, hi = P.d.rank + 1;
+  const bool has_lo = lo >= 0, has_hi = hi < P.d.world;
+  if (!has_lo && !has_hi) return PCS_OK;
+  if (R.group_start() != ncclSuccess) return PCS_ELAUNCH;
+  int bad = 0;
+  for (int k = 0; k < h.nbuf; ++k) {
+    const size_t nb = (size_t)h.bytes[k];
+    if (has_lo) {
+      bad |= R.send(h.send_lo[k], nb, ncclUint8, lo, P.comm, st) != ncclSuccess;
+      bad |= R.recv(h.recv_lo[k], nb, ncclUint8, lo, P.comm, st) != ncclSuccess;
+    }
+    if (has_hi) {
+      bad |= R.send(h.send_hi[k], nb, ncclUint8, hi, P.comm, st) != ncclSuccess;
+      bad |= R.recv(h.recv_hi[k], nb, ncclUint8, hi, P.comm, st) != ncclSuccess;
+    }
+  }
+  bad |= R.group_end() != ncclSuccess;
+  return bad ? PCS_ELAUNCH : PCS_OK;
+}
+
+// all-gather of this rank's 4 sums (parity q) + the loop control over the gathered sums
+static int sums_and_finalize(const Slab2DPlan& P, int q, hipStream_t st) {
+  double* s = P.sums + 4 * q;
+  double* g = P.gathered + 4 * (int64_t)P.d.world * q;
+  if (P.d.world > 1) {
+    if (rccl().all_gather(s, g, 4, ncclFloat64, P.comm, st) != ncclSuccess) return PCS_ELAUNCH;
+  } else {
+    g = s;
+  }
+  return pcs_pds_reduce_finalize(g, P.d.world, P.d.ctrl, P.d.hist, st);
+}
+
+static int run_serial(Slab2DPlan& P, int64_t n, int p0, hipStream_t st) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int p = (int)((p0 + i) & 1);
+    pcs_pds2d_args a = P.d.step[p];
+    a.partials = P.partials;
+    a.hist = nullptr;
+    a.ws = nullptr;
+    int rc = pcs_pds2d_step(&a, st);
+    if (rc == PCS_OK) rc = pcs_reduce_partials(P.partials, P.nfull, P.sums + 4 * p, st);
+    if (rc == PCS_OK) rc = sums_and_finalize(P, p, st);
+    if (rc == PCS_OK) rc = halo_exchange(P, P.d.halo[p], st);
+    if (rc != PCS_OK) return rc;
+  }
+  return PCS_OK;
+}
+
+static int run_overlap(Slab2DPlan& P, int64_t n, int p0, hipStream_t st) {
+  const int64_t R = P.d.step[0].rows, b = P.d.band;
+  // the side stream starts behind everything already queued on the caller's stream
+  if (hipEventRecord(P.ev_fork, st) != hipSuccess || hipStreamWaitEvent(P.side, P.ev_fork, 0) != hipSuccess)
+    return PCS_ELAUNCH;
+  for (int64_t i = 0; i < n; ++i) {
+    const int p = (int)((p0 + i) & 1);
+    pcs_pds2d_args a = P.d.step[p];
+    a.hist = nullptr;
+    a.ws = nullptr;
+    // boundary bands: they read the halo rows of iteration i-1
+    if (i > 0 && hipStreamWaitEvent(st, P.ev_halo, 0) != hipSuccess) return PCS_ELAUNCH;
+    a.partials = P.partials;
+    int rc = pcs_pds2d_step_bands(&a, 0, b, R - b, R, st);
+    if (rc != PCS_OK) return rc;
+    if (hipEventRecord(P.ev_b, st) != hipSuccess) return PCS_ELAUNCH;
+    // side: halo exchange of the boundary rows just written, overlapping the interior
+    if (hipStreamWaitEvent(P.side, P.ev_b, 0) != hipSuccess) return PCS_ELAUNCH;
+    rc = halo_exchange(P, P.d.halo[p], P.side);
+    if (rc != PCS_OK) return rc;
+    if (hipEventRecord(P.ev_halo, P.side) != hipSuccess) return PCS_ELAUNCH;
+    // interior band + this rank's sums
+    a.partials = P.partials + 4 * P.nB;
+    rc = pcs_pds2d_step_bands(&a, b, R - b, R - b, R - b, st);
+    if (rc == PCS_OK) rc = pcs_reduce_partials(P.partials, P.nB + P.nI, P.sums + 4 * p, st);
+    if (rc != PCS_OK) return rc;
+    if (hipEventRecord(P.ev_sum, st) != hipSuccess) return PCS_ELAUNCH;
+    // side: norms across ranks + stopping rule (the next boundary launch does not wait for it)
+    if (hipStreamWaitEvent(P.side, P.ev_sum, 0) != hipSuccess) return PCS_ELAUNCH;
+    rc = sums_and_finalize(P, p, P.side);
+    if (rc != PCS_OK) return rc;
+  }
+  // the caller's stream resumes behind the last halo exchange and loop-control update
+  if (hipEventRecord(P.ev_join, P.side) != hipSuccess || hipStreamWaitEvent(st, P.ev_join, 0) != hipSuccess)
+    return PCS_ELAUNCH;
+  return PCS_OK;
+}
+
+static void destroy_plan(Slab2DPlan* P) {
+  if (!P) return;
+  if (P->side) (void)hipStreamDestroy(P->side);
+  hipEvent_t* evs[] = {&P->ev_fork, &P->ev_b, &P->ev_halo, &P->ev_sum, &P->ev_join};
+  for (hipEvent_t* e : evs)
+    if (*e) (void)hipEventDestroy(*e);
+  if (P->partials) (void)hipFree(P->partials);
+  if (P->sums) (void)hipFree(P->sums);
+  if (P->gathered) (void)hipFree(P->gathered);
+  delete P;
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+extern "C" {
+
+int pcs_comm_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+
+int pcs_comm_available(void) { return rccl().ok ? 1 : 0; }
+
+int pcs_comm_unique_id(void* id) {
+  if (!id) return PCS_EINVAL;
+  if (!rccl().ok) return PCS_EUNSUPPORTED;
+  return rccl().get_unique_id((ncclUniqueId*)id) == ncclSuccess ? PCS_OK : PCS_ELAUNCH;
+}
+
+int pcs_comm_init(const void* id, int world, int rank, void** comm) {
+  if (!id || !comm || world < 1 || rank < 0 || rank >= world) return PCS_EINVAL;
+  if (!rccl().ok) return PCS_EUNSUPPORTED;
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  if (rccl().comm_init_rank(&c, world, uid, rank) != ncclSuccess) return PCS_ELAUNCH;
+  *comm = (void*)c;
+  return PCS_OK;
+}
+
+int pcs_comm_destroy(void* comm) {
+  if (!comm) return PCS_EINVAL;
+  if (!rccl().ok) return PCS_EUNSUPPORTED;
+  return rccl().comm_destroy((ncclComm_t)comm) == ncclSuccess ? PCS_OK : PCS_ELAUNCH;
+}
+
+int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan) {
+  if (!d || !plan || d->world < 1 || d->rank < 0 || d->rank >= d->world || !d->ctrl || !d->hist) return PCS_EINVAL;
+  if (d->world > 1 && (!comm || !rccl().ok)) return PCS_EINVAL;
+  for (int p = 0; p < 2; ++p) {
+    const pcs_halo_set& h = d->halo[p];
+    if (h.nbuf < 0 || h.nbuf > 4) return PCS_EINVAL;
+    for (int k = 0; k < h.nbuf; ++k) {
+      if (h.bytes[k] < 0) return PCS_EINVAL;
+      if (d->rank > 0 && (!h.send_lo[k] || !h.recv_lo[k])) return PCS_EINVAL;
+      if (d->rank < d->world - 1 && (!h.send_hi[k] || !h.recv_hi[k])) return PCS_EINVAL;
+    }
+  }
+  Slab2DPlan* P = new (std::nothrow) Slab2DPlan();
+  if (!P) return PCS_ELAUNCH;
+  P->d = *d;
+  P->comm = (ncclComm_t)comm;
+  pcs_pds2d_args a = d->step[0];
+  a.hist = nullptr;
+  a.ws = nullptr;
+  a.partials = (double*)d->ctrl;  // non-null placeholder for the argument checks
+  P->nfull = pcs_pds2d_nblocks(&a);
+  const int64_t R = a.rows, b = d->band;
+  P->overlap = false;
+  if (d->overlap && b >= 1 && R > 2 * b) {
+    P->nB = pcs_pds2d_nblocks_bands(&a, 0, b, R - b, R);
+    P->nI = pcs_pds2d_nblocks_bands(&a, b, R - b, R - b, R - b);
+    P->overlap = P->nB > 0 && P->nI > 0;
+  }
+  const int64_t np = P->overlap ? P->nB + P->nI : P->nfull;
+  bool ok = P->nfull > 0 && hipMalloc(&P->partials, (size_t)np * 4 * sizeof(double)) == hipSuccess &&
+            hipMalloc(&P->sums, 8 * sizeof(double)) == hipSuccess &&
+            hipMalloc(&P->gathered, (size_t)8 * d->world * sizeof(double)) == hipSuccess;
+  if (ok && P->overlap) {
+    ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess;
+    hipEvent_t* evs[] = {&P->ev_fork, &P->ev_b, &P->ev_halo, &P->ev_sum, &P->ev_join};
+    for (hipEvent_t* e : evs) ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) {
+    destroy_plan(P);
+    return PCS_ELAUNCH;
+  }
+  *plan = P;
+  return PCS_OK;
+}
+
+int pcs_slab2d_overlapped(const void* plan) { return plan && ((const Slab2DPlan*)plan)->overlap ? 1 : 0; }
+
+int pcs_slab2d_run(void* plan, int64_t n, int p0, hipStream_t st) {
+  if (!plan || n < 0 || (p0 != 0 && p0 != 1)) return PCS_EINVAL;
+  Slab2DPlan& P = *(Slab2DPlan*)plan;
+  return P.overlap ? run_overlap(P, n, p0, st) : run_serial(P, n, p0, st);
+}
+
+int pcs_slab2d_destroy(void* plan) {
+  if (!plan) return PCS_EINVAL;
+  destroy_plan((Slab2DPlan*)plan);
+  return PCS_OK;
+}
+
+}  // extern "C"

@@ -56,8 +56,42 @@ class DistComm:
         self.world = dist.get_world_size(group)
         self.staged = dist.get_backend(group) != 'nccl'
 
+        self._native = None
+
     def _peer(self, r):
         return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def native(self):
+        """An RCCL communicator over the same ranks for the native loop (pcs_slab2d_run), or
+        None on a host-staged group or when RCCL could not be bound.  Collective: every
+        rank of the group calls it (the unique id travels over the torch group)."""
+        if self.staged or self.world == 1:
+            return None
+        if self._native is None:
+            lib = L.gpu()
+            ok = torch.tensor([int(lib.pcs_comm_available())], dtype=torch.int32, device='cuda')
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
+            if int(ok.item()) == 0:
+                self._native = False
+                return None
+            nb = int(lib.pcs_comm_id_bytes())
+            uid = (ctypes.c_ubyte * nb)()
+            if self.rank == 0:
+                L.check(lib.pcs_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)), 'pcs_comm_unique_id')
+            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device='cuda')
+            dist.broadcast(t, src=self._peer(0), group=self.group)
+            uid = (ctypes.c_ubyte * nb)(*t.cpu().tolist())
+            h = ctypes.c_void_p()
+            L.check(lib.pcs_comm_init(ctypes.cast(uid, ctypes.c_void_p), self.world, self.rank, ctypes.byref(h)),
+                    'pcs_comm_init')
+            self._native = h
+        return self._native or None
+
+    def close(self):
+        if self._native:
+            torch.cuda.synchronize()
+            L.load().pcs_comm_destroy(self._native)
+        self._native = None
 
     def allgather(self, src, dst):
         """dst[4 r : 4 r + 4] = src of rank r."""
@@ -145,7 +179,8 @@ class SlabPDS2D:
     as [D0 z; D1 z], each ``n0*n1``).  Only this rank's rows (+ halos) are kept.
     """
 
-    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, rank, world, comm=None, chunk=16):
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, rank, world, comm=None, chunk=16, native='auto',
+                 overlap=True):
         self.lib = L.gpu()
         self.comm = comm
         self.rank, self.world = int(rank), int(world)
@@ -205,9 +240,19 @@ class SlabPDS2D:
         self.halos = [lay.halo_pairs([(self.X[q], hx, 0), (self.Z[q], hz, 0), (self.Z[q], hz, 1)]) for q in (0, 1)]
         self.hist = None
         self.chunk = max(1, int(chunk))
+        # native loop (pcs_slab2d_run): one C call per chunk instead of five Python-issued
+        # operations per iteration; needs an RCCL communicator when world > 1
+        if native == 'auto':
+            native = world == 1 or (comm is not None and comm.native() is not None)
+        elif native and world > 1 and (comm is None or comm.native() is None):
+            raise ValueError('native slab loop needs an RCCL (nccl backend) process group')
+        self.native = bool(native)
+        self.overlap = bool(overlap)
+        self._plan = None
+        self._plan_key = None
 
     @classmethod
-    def from_pds(cls, pds, comm, rank=None, world=None, chunk=16):
+    def from_pds(cls, pds, comm, rank=None, world=None, chunk=16, native='auto', overlap=True):
         """This rank's slab of a PDS problem built with the public API on the global image
         (every rank builds the same problem, as a single-host script would)."""
         spec = pds._fused_spec()
@@ -215,7 +260,8 @@ class SlabPDS2D:
             raise ValueError('problem does not match the fused 2-D PDS engine (see opt/engine.match_pds2d)')
         rank = comm.rank if rank is None else rank
         world = comm.world if world is None else world
-        return cls(spec, pds._compute_dtype(), pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank, world, comm, chunk)
+        return cls(spec, pds._compute_dtype(), pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank, world, comm, chunk,
+                   native, overlap)
 
     def _args_for(self, a, p):
         b = L.PdsArgs()
@@ -224,11 +270,82 @@ class SlabPDS2D:
         b.z, b.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
         return b
 
+    # ---- native loop
+    def _halo_set(self, q):
+        """pcs_halo_set of the buffers X[q], Z[q] (written by the step of parity 1 - q)."""
+        hs = L.HaloSet()
+        pairs = self.halos[q]
+        lst = pairs.get(self.rank - 1, []) or pairs.get(self.rank + 1, [])
+        hs.nbuf = len(lst)
+        for side, peer in (('lo', self.rank - 1), ('hi', self.rank + 1)):
+            for k, (snd, rcv) in enumerate(pairs.get(peer, [])):
+                getattr(hs, 'send_' + side)[k] = snd.data_ptr()
+                getattr(hs, 'recv_' + side)[k] = rcv.data_ptr()
+                hs.bytes[k] = snd.numel() * snd.element_size()
+        return hs
+
+    def _native_plan(self):
+        if self.hist is None:
+            self.hist = torch.full((2,), float('nan'), dtype=torch.float64, device=self.X[0].device)
+        key = (self.hist.data_ptr(), self.overlap)
+        if self._plan is not None and self._plan_key == key:
+            return self._plan
+        self._destroy_plan()
+        d = L.Slab2DDesc()
+        d.world, d.rank = self.world, self.rank
+        for p in (0, 1):
+            d.step[p] = self.args[p]
+            d.halo[p] = self._halo_set(1 - p)
+        d.ctrl, d.hist = self.ctrl.data_ptr(), self.hist.data_ptr()
+        d.band = self.hx
+        d.overlap = int(self.overlap)
+        h = ctypes.c_void_p()
+        comm = self.comm.native() if self.world > 1 else None
+        L.check(self.lib.pcs_slab2d_create(ctypes.byref(d), comm, ctypes.byref(h)), 'pcs_slab2d_create')
+        self._desc = d  # keeps the pointers' owners' layout alive with the plan
+        self._plan, self._plan_key = h, key
+        return h
+
+    def _destroy_plan(self):
+        if self._plan is not None:
+            torch.cuda.synchronize()
+            L.load().pcs_slab2d_destroy(self._plan)
+            self._plan = None
+
+    def overlapped(self):
+        """True when the native loop overlaps the halo exchange with the interior band."""
+        return self.native and bool(self.lib.pcs_slab2d_overlapped(self._native_plan()))
+
+    def __del__(self):
+        try:
+            self._destroy_plan()
+        except Exception:
+            pass
+
     # ---- one iteration, split in phases (run_local interleaves them across slabs)
-    def _compute(self, p):
+    def _compute(self, p, split=False):
         st = L.stream()
-        L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args[p]), st), 'pcs_pds2d_step')
-        L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), self.nblocks, L.ptr(self.sums), st),
+        if not split:
+            L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args[p]), st), 'pcs_pds2d_step')
+            L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), self.nblocks, L.ptr(self.sums), st),
+                    'pcs_reduce_partials')
+            return
+        # the native loop's overlapped schedule, serialised: boundary bands, then the interior
+        R, b = self.rows, self.hx
+        bands = [(0, b, R - b, R), (b, R - b, R - b, R - b)]
+        a = L.PdsArgs()
+        ctypes.pointer(a)[0] = self.args[p]
+        nbs = [int(self.lib.pcs_pds2d_nblocks_bands(ctypes.byref(a), *bd)) for bd in bands]
+        if min(nbs) < 0:
+            raise ValueError('banded step needs the row-marching kernels and rows > 2 * halo')
+        if self.partials.numel() < 4 * sum(nbs):
+            self.partials = torch.empty(4 * sum(nbs), dtype=torch.float64, device=self.partials.device)
+        off = 0
+        for bd, nb in zip(bands, nbs):
+            a.partials = self.partials.data_ptr() + 8 * off
+            L.check(self.lib.pcs_pds2d_step_bands(ctypes.byref(a), *bd, st), 'pcs_pds2d_step_bands')
+            off += 4 * nb
+        L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), sum(nbs), L.ptr(self.sums), st),
                 'pcs_reduce_partials')
 
     def _finalize(self):
@@ -261,6 +378,10 @@ class SlabPDS2D:
 
     def advance(self, k):
         """Enqueue k iterations (no host synchronisation)."""
+        if self.native:
+            L.check(self.lib.pcs_slab2d_run(self._native_plan(), int(k), self._p, L.stream()), 'pcs_slab2d_run')
+            self._p ^= int(k) & 1
+            return
         for _ in range(k):
             self.iteration(self._p)
             self._p ^= 1
@@ -309,9 +430,11 @@ class SlabPDS2D:
         return float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
 
-def run_local(slabs, max_iter, min_iter, accuracy_threshold):
+def run_local(slabs, max_iter, min_iter, accuracy_threshold, split=False):
     """Drive all slabs of one image inside one process (device-to-device halo copies);
-    the per-iteration phase order is the distributed one."""
+    the per-iteration phase order is the distributed one.  ``split``: each slab's step runs
+    as the boundary-bands launch + the interior launch (pcs_pds2d_step_bands), as in the
+    native loop's overlapped schedule."""
     total = None
     for s in slabs:
         total = s.init_loop(max_iter, min_iter, accuracy_threshold)
@@ -319,7 +442,7 @@ def run_local(slabs, max_iter, min_iter, accuracy_threshold):
     for i in range(total):
         p = i % 2
         for s in slabs:
-            s._compute(p)
+            s._compute(p, split)
         g = torch.cat([s.sums for s in slabs])
         for s in slabs:
             s.gathered.copy_(g)
