@@ -265,6 +265,14 @@ typedef struct {
 int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a);
 int64_t pcs_pds3d_ws_bytes(const pcs_pds3d_args* a);
 int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t stream);
+/* pcs_pds3d_step restricted to the slab's own planes [a0, b0) u [a1, b1)
+ * (0 <= a0 <= b0 <= a1 <= b1 <= planes): writes x', z' on those planes and one partials row per
+ * block (pcs_pds3d_nblocks_bands of them); hist must be NULL.  Per-voxel arithmetic is that of
+ * the whole-slab step (bitwise the same x', z' for any split).  The multi-GPU loop updates the
+ * boundary bands first, starts their halo exchange, and updates the interior meanwhile. */
+int64_t pcs_pds3d_nblocks_bands(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_t a1, int64_t b1);
+int pcs_pds3d_step_bands(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_t a1, int64_t b1,
+                         hipStream_t stream);
 
 /* Device control block for the hipGraph-captured loop:
  * int32 [0]=it (next iteration), [1]=stopped, [2]=min_iter, [3]=max_iter, [4]=has_dual,

@@ -109,6 +109,8 @@ _SIGS = {
     'pcs_pds3d_nblocks': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_ws_bytes': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_step': (_c_int, [ctypes.POINTER(Pds3Args), _vp]),
+    'pcs_pds3d_nblocks_bands': (_c_i64, [ctypes.POINTER(Pds3Args), _c_i64, _c_i64, _c_i64, _c_i64]),
+    'pcs_pds3d_step_bands': (_c_int, [ctypes.POINTER(Pds3Args), _c_i64, _c_i64, _c_i64, _c_i64, _vp]),
     'pcs_ctrl_bytes': (_c_i64, []),
     'pcs_ctrl_init': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _vp]),
     'pcs_ctrl_init2': (_c_int, [_vp, _c_int, _c_int, _c_dbl, _c_int, _c_int, _vp]),

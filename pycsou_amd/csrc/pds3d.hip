@@ -122,7 +122,7 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
                                                  const T* __restrict__ z, T* __restrict__ zn,
                                                  const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk,
                                                  double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
-                                                 int tiles1, int tiles2, int seg_len, int ntasks) {
+                                                 int tiles1, int tiles2, Bands bd, int ntasks) {
   constexpr int T1 = k3T1, TW = k3TW, NT = k3NT;
   constexpr int UR = T1 + 1, WG = TW + 4, GG = WG / 4;
   constexpr int NU = UR * GG;                 // U items (x_t / u), 153
@@ -148,7 +148,8 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
   const int seg = task / per_plane, t12 = task - seg * per_plane;
   const int ty = t12 / tiles2, tx = t12 - ty * tiles2;
   const int r1 = ty * T1, c2 = tx * TW;
-  const int p_start = seg * seg_len, p_end = min(p_start + seg_len, v.planes);  // own planes [p_start, p_end)
+  int p_start, p_end;  // own planes [p_start, p_end)
+  band_rows(bd, seg, p_start, p_end);
   const int tid = threadIdx.x;
   const int64_t zstride = (int64_t)(v.planes + 2 * v.hz) * v.n1 * v.n2;
   const int64_t pl = (int64_t)v.n1 * v.n2;
@@ -323,29 +324,43 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
 
 // ---------------------------------------------------------------- host side
 struct Plan3 {
-  int tiles1, tiles2, seg_len, nseg, ntasks;
+  int tiles1, tiles2, ntasks;
+  Bands bd;
 };
 
-static Plan3 plan3(const pcs_pds3d_args* a) {
+// own-plane bands [a0, b0) u [a1, b1) of one launch (the whole slab: {0, planes, planes, planes})
+struct PlaneBands {
+  int64_t a0, b0, a1, b1;
+};
+
+static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   Plan3 p;
+  if (pb.b0 == pb.a0) pb = PlaneBands{pb.a1, pb.b1, pb.b1, pb.b1};
   p.tiles1 = (int)((a->n1 + k3T1 - 1) / k3T1);
   p.tiles2 = (int)((a->n2 + k3TW - 1) / k3TW);
   const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
+  const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
+  const int64_t bands = (L0 > 0) + (L1 > 0);
   // about 8 resident workgroups per CU on 256 CUs; never segments shorter than 8 planes
   int64_t nseg = (2048 + per_plane - 1) / per_plane;
-  const int64_t max_seg = (a->planes + 7) / 8;
-  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
-  p.seg_len = (int)((a->planes + nseg - 1) / nseg);
-  p.nseg = (int)((a->planes + p.seg_len - 1) / p.seg_len);
-  p.ntasks = (int)(per_plane * p.nseg);
+  const int64_t max_seg = (L + 7) / 8;
+  nseg = nseg > max_seg ? max_seg : nseg;
+  nseg = nseg < bands ? bands : nseg;
+  nseg = nseg < 1 ? 1 : nseg;
+  const int64_t seg_len = (L + nseg - 1) / nseg;
+  const int64_t n0 = seg_len ? (L0 + seg_len - 1) / seg_len : 0, n1 = seg_len ? (L1 + seg_len - 1) / seg_len : 0;
+  p.bd = Bands{(int)seg_len, (int)n0, (int)pb.a0, (int)pb.b0, (int)pb.a1, (int)pb.b1};
+  p.ntasks = (int)(per_plane * (n0 + n1));
   return p;
 }
+static PlaneBands full3(const pcs_pds3d_args* a) { return PlaneBands{0, a->planes, a->planes, a->planes}; }
 
 static bool aligned16_3(const void* q) { return q == nullptr || ((uintptr_t)q & 15) == 0; }
 
 template <typename T, int FK, bool VEC>
-static int launch3(const pcs_pds3d_args* a, hipStream_t st) {
-  const Plan3 p = plan3(a);
+static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
+  const Plan3 p = plan3(a, pb);
+  if (p.ntasks == 0) return PCS_OK;
   Vol v;
   v.n0 = (int)a->n0;
   v.n1 = (int)a->n1;
@@ -375,26 +390,26 @@ static int launch3(const pcs_pds3d_args* a, hipStream_t st) {
   P.seg_b = (T)a->seg_b;
   k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, k3NT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn,
                                                       (const T*)a->g, v, P, a->hkind, a->gkind, a->partials,
-                                                      (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.seg_len,
+                                                      (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.bd,
                                                       p.ntasks);
   return launch_status();
 }
 
 template <typename T, bool VEC>
-static int pds3d_v(const pcs_pds3d_args* a, hipStream_t st) {
+static int pds3d_v(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   switch (a->fkind) {
-    case PCS_F_NULL: return launch3<T, PCS_F_NULL, VEC>(a, st);
-    case PCS_F_DENOISE: return launch3<T, PCS_F_DENOISE, VEC>(a, st);
-    case PCS_F_GRADBUF: return launch3<T, PCS_F_GRADBUF, VEC>(a, st);
+    case PCS_F_NULL: return launch3<T, PCS_F_NULL, VEC>(a, pb, st);
+    case PCS_F_DENOISE: return launch3<T, PCS_F_DENOISE, VEC>(a, pb, st);
+    case PCS_F_GRADBUF: return launch3<T, PCS_F_GRADBUF, VEC>(a, pb, st);
     default: return PCS_EINVAL;
   }
 }
 
 template <typename T>
-static int pds3d(const pcs_pds3d_args* a, hipStream_t st) {
+static int pds3d(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   const bool vec = a->n2 % 4 == 0 && aligned16_3(a->x) && aligned16_3(a->xn) && aligned16_3(a->z) &&
                    aligned16_3(a->zn) && aligned16_3(a->g);
-  return vec ? pds3d_v<T, true>(a, st) : pds3d_v<T, false>(a, st);
+  return vec ? pds3d_v<T, true>(a, pb, st) : pds3d_v<T, false>(a, pb, st);
 }
 
 }  // namespace pcs
@@ -405,7 +420,7 @@ extern "C" {
 
 int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a) {
   if (!a || a->planes < 1 || a->n1 < 1 || a->n2 < 1) return -1;
-  return plan3(a).ntasks;
+  return plan3(a, full3(a)).ntasks;
 }
 
 int64_t pcs_pds3d_ws_bytes(const pcs_pds3d_args* a) {
@@ -413,7 +428,7 @@ int64_t pcs_pds3d_ws_bytes(const pcs_pds3d_args* a) {
   return nb < 0 ? -1 : red_ws_bytes(nb);
 }
 
-int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t st) {
+static int check3(const pcs_pds3d_args* a) {
   if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
   if (a->n0 < 1 || a->n1 < 1 || a->n2 < 1 || a->planes < 1 || a->plane0 < 0 || a->plane0 + a->planes > a->n0)
     return PCS_EINVAL;
@@ -427,9 +442,35 @@ int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t st) {
   const int64_t esz = a->dtype == PCS_F64 ? 8 : 4;
   if (a->n1 * a->n2 * esz > (1LL << 30) || a->n0 >= (1LL << 30)) return PCS_EUNSUPPORTED;  // one plane <= 1 GiB
   if (a->hist && (!a->ws || !a->ctrl || !aligned16_3(a->ws) || !aligned16_3(a->partials))) return PCS_EINVAL;
-  if (a->dtype == PCS_F32) return pds3d<float>(a, st);
-  if (a->dtype == PCS_F64) return pds3d<double>(a, st);
-  return PCS_EINVAL;
+  if (a->dtype != PCS_F32 && a->dtype != PCS_F64) return PCS_EINVAL;
+  return PCS_OK;
 }
+
+static int step3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
+  return a->dtype == PCS_F32 ? pds3d<float>(a, pb, st) : pds3d<double>(a, pb, st);
+}
+
+static bool bands3_ok(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_t a1, int64_t b1) {
+  return 0 <= a0 && a0 <= b0 && b0 <= a1 && a1 <= b1 && b1 <= a->planes;
+}
+
+int pcs_pds3d_step(const pcs_pds3d_args* a, hipStream_t st) {
+  const int rc = check3(a);
+  return rc != PCS_OK ? rc : step3(a, full3(a), st);
+}
+
+int64_t pcs_pds3d_nblocks_bands(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_t a1, int64_t b1) {
+  if (check3(a) != PCS_OK || !bands3_ok(a, a0, b0, a1, b1)) return -1;
+  return plan3(a, PlaneBands{a0, b0, a1, b1}).ntasks;
+}
+
+int pcs_pds3d_step_bands(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_t a1, int64_t b1, hipStream_t st) {
+  const int rc = check3(a);
+  if (rc != PCS_OK) return rc;
+  if (a->hist || !bands3_ok(a, a0, b0, a1, b1)) return PCS_EINVAL;
+  return step3(a, PlaneBands{a0, b0, a1, b1}, st);
+}
+
+
 
 }  // extern "C"

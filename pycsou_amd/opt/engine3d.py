@@ -98,7 +98,8 @@ def match_pds3d(F, G, H, K, has_H):
 class PDS3DEngine:
     """Device state + loop of one rank's slab (the whole volume when world == 1)."""
 
-    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, comm=None, rank=0, world=1, chunk=8, use_graph=True):
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, comm=None, rank=0, world=1, chunk=8, use_graph=True,
+                 overlap=True):
         self.lib = L.gpu()
         self.spec, self.dtype, self.comm = spec, dtype, comm
         self.rank, self.world = int(rank), int(world)
@@ -158,6 +159,20 @@ class PDS3DEngine:
             else:
                 # the chain's final buffer is fixed by its length: forward + adjoint passes
                 self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
+        # Banded schedule (multi-GPU): the update of the B = hx + 1 planes at each end of the slab
+        # (the planes the neighbours' halos copy, and the only ones whose gradient reaches into
+        # our halos) runs first, their halo exchange overlaps the interior update, and the
+        # in-plane passes of our own planes run before the previous exchange is awaited.
+        # Needs the fused axis-0 gradient with both in-plane passes in one launch (C4/C5).
+        self.band = hx + 1
+        self.banded = (fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and world > 1
+                       and self.rows > 2 * self.band) if fk == L.PCS_F_GRADBUF else False
+        self.overlap = bool(overlap)
+        if fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and self.rows > 2 * self.band:
+            # g in a buffer of its own: the banded order writes g on the boundary planes while the
+            # interior's axis-0 pass still reads the in-plane forward result around them
+            self.T.append(torch.empty_like(self.T[0]))
+            self.gbuf = self.T[2]
         a = L.Pds3Args()
         a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
         a.fkind, a.hkind, a.gkind = fk, spec['hkind'], spec['gkind']
@@ -237,11 +252,9 @@ class PDS3DEngine:
         dims = L.i64s((q1 - q0, self.n1, self.n2))
         esz = cur.element_size()
         if self.sep2:
-            dst = self.T[j % 2]
+            dst = self.gbuf
             self._sep_planes(ctypes.c_void_p(cur.data_ptr() + q0 * plane * esz),
                              ctypes.c_void_p(dst.data_ptr() + q0 * plane * esz), q1 - q0, self.inplane[::-1], True, st)
-            cur = dst
-            assert cur is self.gbuf
             return
         for axis, _, hf, k, off in reversed(self.inplane):
             dst = self.T[j % 2]
@@ -250,6 +263,70 @@ class PDS3DEngine:
                                         L.ptr(hf), int(k), int(k - 1 - off), st), 'pcs_conv1d')
             cur, j = dst, j + 1
         assert cur is self.gbuf
+
+    # ---- banded order (sep2 + fused axis-0 pass): planes in sub-volume coordinates
+    def _sep_range(self, src, dst, j0, j1, flipped, st):
+        if j1 <= j0:
+            return
+        off = j0 * self.plane * src.element_size()
+        ops = self.inplane[::-1] if flipped else self.inplane
+        self._sep_planes(ctypes.c_void_p(src.data_ptr() + off), ctypes.c_void_p(dst.data_ptr() + off), j1 - j0, ops,
+                         flipped, st)
+
+    def _g_range(self, q0, q1, st):
+        """g = C^T (C x - y) on sub-volume planes [q0, q1) from the in-plane result in T0."""
+        if q1 <= q0:
+            return
+        nsub = self.rows + 2 * self.hx
+        img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0
+        _, h, _, k, off = self.ax0
+        L.check(self.lib.pcs_conv0_residual_adjoint(self.base_args.dtype, L.ptr(self.T[0]), L.ptr(self.yw),
+                                                    L.ptr(self.T[1]), nsub, self.plane, L.ptr(h), int(k), int(off),
+                                                    img_lo, img_hi, q0, q1, st), 'pcs_conv0_residual_adjoint')
+        self._sep_range(self.T[1], self.gbuf, q0, q1, True, st)
+
+    def _band_pre(self, p, st):
+        """In-plane forward passes of the own planes (no halo needed)."""
+        self._sep_range(self.X[p], self.T[0], self.hx, self.hx + self.rows, False, st)
+
+    def _band_boundary(self, p, st):
+        """In-plane passes of the halo planes, g and the update on the two boundary bands."""
+        hx, R, B = self.hx, self.rows, self.band
+        nsub = R + 2 * hx
+        self._sep_range(self.X[p], self.T[0], 0, hx, False, st)
+        self._sep_range(self.X[p], self.T[0], hx + R, nsub, False, st)
+        self._g_range(hx, hx + B + 1, st)
+        self._g_range(hx + R - B, min(hx + R + 1, nsub), st)
+        a = self.args[p]
+        a.hist = None
+        a.partials = self.partials.data_ptr()
+        L.check(self.lib.pcs_pds3d_step_bands(ctypes.byref(a), 0, B, R - B, R, st), 'pcs_pds3d_step_bands')
+
+    def _band_interior(self, p, st):
+        hx, R, B = self.hx, self.rows, self.band
+        self._g_range(hx + B + 1, hx + R - B, st)
+        a = self.args[p]
+        a.hist = None
+        a.partials = self.partials.data_ptr() + 32 * self.nb_bands[0]
+        L.check(self.lib.pcs_pds3d_step_bands(ctypes.byref(a), B, R - B, R - B, R - B, st), 'pcs_pds3d_step_bands')
+        a.partials = self.partials.data_ptr()
+        L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), sum(self.nb_bands), L.ptr(self.sums), st),
+                'pcs_reduce_partials')
+
+    def _init_bands(self):
+        if getattr(self, 'nb_bands', None) is not None:
+            return
+        R, B = self.rows, self.band
+        a = self.args[0]
+        self.nb_bands = [int(self.lib.pcs_pds3d_nblocks_bands(ctypes.byref(a), 0, B, R - B, R)),
+                         int(self.lib.pcs_pds3d_nblocks_bands(ctypes.byref(a), B, R - B, R - B, R - B))]
+        if min(self.nb_bands) < 1:
+            raise ValueError('banded 3-D step unavailable for this slab')
+        need = 4 * sum(self.nb_bands)
+        if self.partials.numel() < need:
+            self.partials = torch.empty(need, dtype=torch.float64, device=self.partials.device)
+            for q in (0, 1):
+                self.args[q].partials = self.partials.data_ptr()
 
     def _gradient(self, p, st):
         if self.fused0:
@@ -285,7 +362,14 @@ class PDS3DEngine:
         L.check(self.lib.pcs_pds3d_step(ctypes.byref(a), st), 'pcs_pds3d_step')
 
     # phases of a multi-rank iteration (pycsou_amd.parallel.run_local interleaves them)
-    def _compute(self, p):
+    def _compute(self, p, split=False):
+        if split:  # the banded order, serialised (run_local)
+            self._init_bands()
+            st = L.stream()
+            self._band_pre(p, st)
+            self._band_boundary(p, st)
+            self._band_interior(p, st)
+            return
         self._step(p, None)
         L.check(self.lib.pcs_reduce_partials(L.ptr(self.partials), self.nblocks, L.ptr(self.sums), L.stream()),
                 'pcs_reduce_partials')
@@ -298,10 +382,33 @@ class PDS3DEngine:
         if self.world == 1:
             self._step(p, self.hist)
             return
+        if self.banded and self.overlap:
+            # in-plane passes of our planes overlap the previous iteration's halo exchange and
+            # sums all-gather; the boundary bands' exchange overlaps the interior update
+            self._init_bands()
+            st = L.stream()
+            self._band_pre(p, st)
+            self._drain()
+            self._band_boundary(p, st)
+            self._pending_ex = self.comm.exchange_start(self.halos[1 - p])
+            self._band_interior(p, st)
+            self._pending_ag = self.comm.allgather_start(self.sums, self.gathered)
+            return
         self._compute(p)
         self.comm.allgather(self.sums, self.gathered)
         self._finalize()
         self.comm.exchange(self.halos[1 - p])
+
+    def _drain(self):
+        """Order the current stream after the in-flight exchange / all-gather and run the loop
+        control of the iteration they belong to."""
+        ex, ag = getattr(self, '_pending_ex', None), getattr(self, '_pending_ag', None)
+        self._pending_ex = self._pending_ag = None
+        if ex is not None:
+            ex.wait()
+        if ag is not None:
+            ag.wait()
+            self._finalize()
 
     # ---- loops
     def init_loop(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
@@ -335,6 +442,7 @@ class PDS3DEngine:
         for _ in range(k):
             self.iteration(self._p)
             self._p ^= 1
+        self._drain()
 
     def iterations(self):
         return int(self.ctrl.view(torch.int32)[0].item())

@@ -104,6 +104,26 @@ class DistComm:
         else:
             dist.all_gather_into_tensor(dst, src, group=self.group)
 
+    def allgather_start(self, src, dst):
+        """allgather() without waiting: RCCL runs it on its own stream behind the work queued
+        so far; the handle's wait() orders the current stream after it."""
+        if self.world == 1 or self.staged:
+            self.allgather(src, dst)
+            return _Done()
+        return _Works([dist.all_gather_into_tensor(dst, src, group=self.group, async_op=True)])
+
+    def exchange_start(self, pairs):
+        """exchange() without waiting (see allgather_start)."""
+        if not pairs or self.staged:
+            self.exchange(pairs)
+            return _Done()
+        ops = []
+        for peer, lst in sorted(pairs.items()):
+            for snd, rcv in lst:
+                ops.append(dist.P2POp(dist.isend, snd, self._peer(peer), self.group))
+                ops.append(dist.P2POp(dist.irecv, rcv, self._peer(peer), self.group))
+        return _Works(dist.batch_isend_irecv(ops))
+
     def exchange(self, pairs):
         """pairs: {peer: [(send_view, recv_view), ...]}; the k-th send to a peer lands in the
         peer's k-th receive from us."""
@@ -132,6 +152,25 @@ class DistComm:
                 ops.append(dist.P2POp(dist.irecv, r, self._peer(peer), self.group))
         for q in dist.batch_isend_irecv(ops):
             q.wait()
+
+
+class _Done:
+    """Handle of a transfer that completed inside its start call (host-staged transport)."""
+
+    def wait(self):
+        pass
+
+
+class _Works:
+    """Handle of in-flight torch.distributed (NCCL = RCCL) operations: wait() makes the
+    current stream wait for them (no host synchronisation)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
 
 
 class SlabLayout:
