@@ -20,6 +20,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -112,7 +113,13 @@ def slab_bench(n, dtype, K, W, world):
     from pycsou_amd.parallel import DistComm, SlabPDS2D
     pds = build_problem(n * world, n, dtype)
     comm = DistComm() if world > 1 else None
-    eng = SlabPDS2D.from_pds(pds, comm, rank=0 if comm is None else None, world=1 if comm is None else None)
+    kw = dict(rank=0 if comm is None else None, world=1 if comm is None else None)
+    try:  # the native loop (RCCL bound by the library) unless it cannot be set up on this box
+        eng = SlabPDS2D.from_pds(pds, comm, native=True, **kw)
+        eng.overlapped()
+    except Exception as e:  # noqa: BLE001 -- the torch.distributed-issued loop runs the same kernels
+        print(f'bench: native slab loop unavailable ({e}); torch.distributed per-iteration loop', file=sys.stderr)
+        eng = SlabPDS2D.from_pds(pds, comm, native=False, **kw)
     del pds
     torch.cuda.empty_cache()
     total = W + K + 4
@@ -138,7 +145,9 @@ def slab_bench(n, dtype, K, W, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
-    return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks}
+    loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else 'python'
+    return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks,
+            'loop': loop}
 
 
 def main():
@@ -218,7 +227,8 @@ def main():
                                    + (f'chunks of {chunk} iterations launched from C (pcs_pds2d_run)'
                                       if 'nblocks' in res and world == 1
                                       and args.engine != 'slab' else
-                                      'slab engine: per-iteration RCCL all-gather of 4 sums + halo exchange'),
+                                      f'slab engine ({res.get("loop", "python")} loop): per-iteration RCCL '
+                                      f'all-gather of 4 sums + neighbour halo exchange'),
                        'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,

@@ -7,6 +7,11 @@ through the public API and run by PDS3DEngine (hipGraph chunks).  Prints one JSO
 it/s, ms per iteration, the update kernel's mean duration and the algorithmic rates.
 
   python tools/bench3d.py --size 512 --dtype f32 --steps 20 --warmup 4
+
+--rank-of W: time ONE rank's share of a W-GPU plane-slab run on this GPU (a middle rank:
+both halos), with a transport that moves nothing (halo planes stay stale; per-iteration
+compute is what is measured), in the serial order and in the banded order of the multi-GPU
+loop.  The halo bytes per side per iteration are printed beside it.
 """
 import argparse
 import json
@@ -45,11 +50,13 @@ def build(n, dtype, seed=0):
     C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
     y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
     del xs
+    print('  blurred data ready', flush=True)
     K = Gradient(shape=shape, kind='forward')
     K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(sum(4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2
                                                                for _ in range(3))))
     F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
     H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
+    print('  functionals ready', flush=True)
     return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
                z0=torch.zeros(3 * N, dtype=dtype, device='cuda'), verbose=None)
 
@@ -60,7 +67,10 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=4)
+    ap.add_argument('--rank-of', type=int, default=0)
     args = ap.parse_args()
+    if args.rank_of > 1:
+        return rank_share(args)
     torch.cuda.set_device(0)
     dtype = torch.float32 if args.dtype == 'f32' else torch.float64
     from pycsou_amd.opt.engine3d import PDS3DEngine
@@ -92,6 +102,64 @@ def main():
                       'update_kernel_ms': round(kms, 4), 'alg_bytes_per_iter': alg,
                       'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
                       'update_kernel_GBps': round(alg / (kms * 1e-3) / 1e9, 1), 'setup_s': round(time.time() - t0, 1)}))
+
+
+class NullComm:
+    """Transport stand-in for timing one rank alone: no data moves."""
+    staged = True
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    def allgather(self, src, dst):
+        dst[:4].copy_(src)
+
+    def exchange(self, pairs):
+        pass
+
+    def allgather_start(self, src, dst):
+        self.allgather(src, dst)
+        return self
+
+    def exchange_start(self, pairs):
+        return self
+
+    def wait(self):
+        pass
+
+
+def rank_share(args):
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    torch.cuda.set_device(0)
+    dtype = torch.float32 if args.dtype == 'f32' else torch.float64
+    W = args.rank_of
+    rank = W // 2 - 1 if W > 2 else 0
+    t0 = time.time()
+    print(f'building {args.size}^3 ...', flush=True)
+    pds = build(args.size, dtype)
+    spec = pds._fused_spec()
+    print(f'built in {time.time() - t0:.1f} s', flush=True)
+    K = args.steps + args.steps % 2
+    out = {'workload': f'one rank ({rank} of {W}) of 3-D TV-deconv {args.size}^3 {args.dtype}'}
+    for name, ov in (('serial', False), ('banded', True)):
+        eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, comm=NullComm(rank, W),
+                          rank=rank, world=W, overlap=ov)
+        eng.init_loop(K + 8, K + 8, -1.0)
+        eng.advance(4)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        eng.advance(K)
+        e1.record()
+        torch.cuda.synchronize()
+        out[f'{name}_ms_per_iter'] = round(e0.elapsed_time(e1) / K, 4)
+        out['planes'], out['banded'] = eng.rows, bool(eng.banded)
+        print(name, out[f'{name}_ms_per_iter'], 'ms/iter', flush=True)
+        esz = eng.X[0].element_size()
+        out['halo_bytes_per_side'] = (eng.hx + 3 * eng.hz) * eng.plane * esz
+        del eng
+        torch.cuda.empty_cache()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == '__main__':
