@@ -141,7 +141,7 @@ def slab_bench(n, dtype, K, W, world):
     it_done = eng.iterations()
     assert it_done == W + K, (it_done, W, K)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda' if dist.get_backend() == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
@@ -166,9 +166,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # PCS_BENCH_BACKEND=gloo + several ranks on one GPU: a rehearsal of the N > 1 code path on a
+    # one-GPU box (host-staged transport; the timing is not a scaling number)
+    backend = os.environ.get('PCS_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dtype = torch.float32 if args.dtype == 'f32' else torch.float64
     n = args.size
     K = max(2, args.steps + (args.steps % 2))
