@@ -51,6 +51,14 @@ int pcs_deriv1_fwd(int dtype, const void* x, void* out, int ndim, const int64_t*
 int pcs_deriv1_adj(int dtype, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step,
                    int kind, int edge, hipStream_t stream);
 
+/* SecondDerivative along `axis` (pycsou/linop/diff.py:133-219 -> pylops.SecondDerivative):
+ * out[i] = (x[i+1] - 2 x[i] + x[i-1]) / step^2 inside; ends 0, or the one-sided second-order
+ * stencils with `edge`.  ndim in 1..3. */
+int pcs_deriv2_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step,
+                   int edge, hipStream_t stream);
+int pcs_deriv2_adj(int dtype, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step,
+                   int edge, hipStream_t stream);
+
 /* Gradient (pycsou/linop/diff.py:777-882 -> pylops.Gradient = VStack of FirstDerivative):
  * out[k*N:(k+1)*N] = D_k x for k < ndim.  steps[ndim]. */
 int pcs_grad_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, const double* steps,
@@ -97,6 +105,14 @@ int pcs_conv2d_sep_planes(int dtype, const void* in, void* out, int64_t nplanes,
 int pcs_conv0_residual_adjoint(int dtype, const void* t, const void* y, void* s, int64_t nsub, int64_t plane,
                                const void* taps, int k, int off, int64_t img_lo, int64_t img_hi, int64_t q0,
                                int64_t q1, hipStream_t stream);
+
+/* Masking / DownSampling / SubSampling (pycsou/linop/sampling.py:25-391).
+ * pcs_gather:          out[i] = x[idx[i]], i < m         (Masking.__call__, sampling.py:192-193)
+ * pcs_gather_or_zero:  out[p] = inv[p] >= 0 ? y[inv[p]] : 0, p < n
+ *                      = (x = 0; x[idx] = y) with inv the inverse index map (Masking.adjoint,
+ *                      sampling.py:195-198).  Indices are int32 (n < 2^31). */
+int pcs_gather(int dtype, const void* x, const int32_t* idx, void* out, int64_t m, hipStream_t stream);
+int pcs_gather_or_zero(int dtype, const void* y, const int32_t* inv, void* out, int64_t n, hipStream_t stream);
 
 /* ---------------------------------------------------------------- prox / functionals */
 

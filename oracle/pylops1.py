@@ -12,6 +12,9 @@ PyLops (``pylops >= 1.9.2``, 1.x keyword API) is not vendored under
 * ``pycsou/linop/diff.py:957``  ``pylops.Laplacian(dims, weights, sampling, edge, dtype)``
 * ``pycsou/linop/conv.py:163``  ``pylops.signalprocessing.Convolve1D(N, h, dims, dir, dtype, method, offset)``
 * ``pycsou/linop/conv.py:294``  ``pylops.signalprocessing.Convolve2D(N, h, dims, nodir, dtype, method, offset)``
+* ``pycsou/linop/conv.py:358``  ``pylops.Smoothing1D(nsmooth, dims, dir, dtype)``
+* ``pycsou/linop/conv.py:417``  ``pylops.Smoothing2D(nsmooth, dims, nodir, dtype)``
+* ``pycsou/linop/sampling.py:121``  ``pylops.Restriction(M, iava, dims, dir, dtype, inplace)``
 
 Every object exposes ``shape``, ``dtype``, ``explicit``, ``matvec`` and
 ``rmatvec`` -- the attributes pycsou's ``PyLopLinearOperator``
@@ -259,3 +262,47 @@ def pycsou_offset(n):
     """Offset pycsou passes to PyLops for a filter of length n
     (``pycsou/linop/conv.py:159-162, 285-292``)."""
     return n // 2 - 1 if n % 2 == 0 else n // 2
+
+
+def Smoothing1D(nsmooth, dims, dir=0, dtype='float64'):
+    """PyLops 1.x ``Smoothing1D``: an even ``nsmooth`` is raised by one; ``Convolve1D`` with
+    ``ones(nsmooth) / nsmooth`` and offset ``(nsmooth - 1) / 2``."""
+    dims = (int(dims),) if np.isscalar(dims) else tuple(int(d) for d in dims)
+    if nsmooth % 2 == 0:
+        nsmooth += 1
+    return Convolve1D(int(np.prod(dims)), np.ones(nsmooth) / float(nsmooth), offset=(nsmooth - 1) // 2, dims=dims,
+                      dir=dir, dtype=dtype)
+
+
+def Smoothing2D(nsmooth, dims, nodir=None, dtype='float64'):
+    """PyLops 1.x ``Smoothing2D``: box filter ``ones(n0, n1) / (n0 n1)`` (even sizes raised by
+    one), centred, via ``Convolve2D``."""
+    n = [int(v) for v in nsmooth]
+    n = [v + 1 if v % 2 == 0 else v for v in n]
+    h = np.ones((n[0], n[1])) / float(n[0] * n[1])
+    dims = tuple(int(d) for d in dims)
+    return Convolve2D(int(np.prod(dims)), h, dims, offset=((n[0] - 1) // 2, (n[1] - 1) // 2), nodir=nodir,
+                      dtype=dtype)
+
+
+class Restriction(_Op):
+    """PyLops 1.x ``Restriction``: ``y = x.take(iava, axis=dir)``; adjoint ``x = 0;
+    x[..., iava, ...] = y`` along ``dir``."""
+
+    def __init__(self, M, iava, dims=None, dir=0, dtype='float64', inplace=True):
+        self.iava = np.asarray(iava, dtype=np.int64).ravel()
+        self.dims = (int(M),) if dims is None else tuple(int(d) for d in dims)
+        self.dir = int(dir)
+        out = list(self.dims)
+        out[self.dir] = self.iava.size
+        self.dimsd = tuple(out)
+        super().__init__((int(np.prod(self.dimsd)), int(M)), dtype)
+
+    def matvec(self, x):
+        return np.take(np.reshape(x, self.dims), self.iava, axis=self.dir).ravel()
+
+    def rmatvec(self, y):
+        y = np.swapaxes(np.reshape(y, self.dimsd), self.dir, 0)
+        x = np.zeros(np.swapaxes(np.zeros(self.dims, bool), self.dir, 0).shape, dtype=self.dtype)
+        x[self.iava] = y
+        return np.ascontiguousarray(np.swapaxes(x, 0, self.dir)).ravel()

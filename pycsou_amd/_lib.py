@@ -66,6 +66,10 @@ _SIGS = {
     'pcs_abi_version': (_c_int, []),
     'pcs_deriv1_fwd': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _c_int, _vp]),
     'pcs_deriv1_adj': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _c_int, _vp]),
+    'pcs_deriv2_fwd': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _vp]),
+    'pcs_deriv2_adj': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _c_dbl, _c_int, _vp]),
+    'pcs_gather': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _vp]),
+    'pcs_gather_or_zero': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _vp]),
     'pcs_grad_fwd': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _pdbl, _c_int, _c_int, _vp]),
     'pcs_grad_adj': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _pdbl, _c_int, _c_int, _vp]),
     'pcs_lap_fwd': (_c_int, [_c_int, _vp, _vp, _pi64, _pdbl, _pdbl, _c_int, _vp]),

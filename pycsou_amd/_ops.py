@@ -227,6 +227,32 @@ def deriv1(x, dims, axis, step, kind, edge, adjoint=False):
     return out
 
 
+def deriv2(x, dims, axis, step, edge, adjoint=False):
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    fn = lib.pcs_deriv2_adj if adjoint else lib.pcs_deriv2_fwd
+    L.check(fn(L.dtcode(x), L.ptr(x), L.ptr(out), len(dims), L.i64s(dims), int(axis), float(step), int(bool(edge)),
+               L.stream()), 'pcs_deriv2')
+    return out
+
+
+def gather(x, idx):
+    """x[idx] (idx: int32 device tensor)."""
+    lib = L.gpu()
+    out = torch.empty(idx.numel(), dtype=x.dtype, device=x.device)
+    L.check(lib.pcs_gather(L.dtcode(x), L.ptr(x), L.ptr(idx), L.ptr(out), idx.numel(), L.stream()), 'pcs_gather')
+    return out
+
+
+def gather_or_zero(y, inv):
+    """out[p] = y[inv[p]] if inv[p] >= 0 else 0 (inv: int32 device tensor)."""
+    lib = L.gpu()
+    out = torch.empty(inv.numel(), dtype=y.dtype, device=y.device)
+    L.check(lib.pcs_gather_or_zero(L.dtcode(y), L.ptr(y), L.ptr(inv), L.ptr(out), inv.numel(), L.stream()),
+            'pcs_gather_or_zero')
+    return out
+
+
 def lap(x, dims, weights, steps, edge, adjoint=False):
     lib = L.gpu()
     out = torch.empty_like(x)

@@ -318,3 +318,137 @@ class DiffMapComp(MapComp, DifferentiableMap):
         else:
             j1 = self.map1._jacT(self.map2._apply(t))
         return _mul(j2, j1)
+
+
+# ---------------------------------------------------------------- stacks (map.py:613-958)
+def _sections(block_sizes):
+    """Offsets of ``np.split(x, np.cumsum(block_sizes))``: block i is ``[o[i], o[i+1])``."""
+    return [0] + [int(s) for s in np.cumsum(block_sizes)]
+
+
+def _as_flat(v, like):
+    """A block result as a flat device tensor (functionals return numbers)."""
+    if isinstance(v, torch.Tensor):
+        return v.reshape(-1)
+    return torch.as_tensor(np.asarray(v, dtype=np.float64).reshape(-1), device=like.device,
+                           dtype=like.dtype if like.dtype.is_floating_point else torch.float64)
+
+
+def _cat(parts, like):
+    """np.concatenate of flat device blocks into one new buffer (one copy per block)."""
+    parts = [_as_flat(p, like) for p in parts]
+    out = torch.empty(sum(p.numel() for p in parts), dtype=parts[0].dtype, device=parts[0].device)
+    o = 0
+    for p in parts:
+        out[o:o + p.numel()].copy_(p)
+        o += p.numel()
+    return out
+
+
+class MapStack(Map):
+    """Vertical (``axis=0``: ``x -> (f_1(x), ..., f_k(x))``) or horizontal (``axis=1``:
+    ``(x_1, ..., x_k) -> sum_i f_i(x_i)``) stacking (``map.py:613-743``).  The blocks run one
+    after the other on the current stream; ``n_jobs`` / ``joblib_backend`` are accepted for
+    API compatibility (the reference's joblib fan-out has no GPU counterpart)."""
+
+    def __init__(self, *maps, axis, n_jobs=1, joblib_backend='loky'):
+        self.maps = list(maps)
+        if np.abs(axis) > 1:
+            ValueError('Axis must be one of {0, 1,-1}.')  # the reference builds but does not raise (map.py:703-704)
+        self.axis = int(axis)
+        self.is_linear_list = [m.is_linear for m in self.maps]
+        self.is_differentiable_list = [m.is_differentiable for m in self.maps]
+        self.shapes = np.array([m.shape for m in self.maps])
+        self.block_sizes = [m.shape[axis] for m in self.maps]
+        self.sections = np.cumsum(self.block_sizes)
+        self._off = _sections(self.block_sizes)
+        self.n_jobs = n_jobs
+        self.joblib_backend = joblib_backend
+        if not self.is_valid_stack():
+            raise ValueError('Inconsistent map shapes for  stacking.')
+        Map.__init__(self, shape=self.get_shape(), is_linear=bool(np.prod(self.is_linear_list).astype(bool)),
+                     is_differentiable=bool(np.prod(self.is_differentiable_list).astype(bool)))
+
+    def is_valid_stack(self):
+        col_sizes = [m.shape[1 - self.axis] for m in self.maps]
+        return np.unique(col_sizes).size == 1
+
+    def get_shape(self):
+        sizes = [m.shape[self.axis] for m in self.maps]
+        if self.axis == 0:
+            return int(np.sum(sizes).astype(int)), self.maps[0].shape[1 - self.axis]
+        return self.maps[0].shape[1 - self.axis], int(np.sum(sizes).astype(int))
+
+    def _split(self, t):
+        o = self._off
+        return [t[o[i]:o[i + 1]] for i in range(len(self.maps))]
+
+    def _apply(self, t):
+        if self.axis == 0:
+            return _cat([m._apply(t) for m in self.maps], t)
+        result = 0
+        for m, xi in zip(self.maps, self._split(t)):
+            r = m._apply(xi)
+            if isinstance(result, torch.Tensor) and isinstance(r, torch.Tensor):
+                result = O.add(result, r)
+            else:
+                result = result + r
+        return result
+
+
+class MapVStack(MapStack):
+    """``MapStack(*maps, axis=0)`` (``map.py:746-780``)."""
+
+    def __init__(self, *maps, n_jobs=1, joblib_backend='loky'):
+        super().__init__(*maps, axis=0, n_jobs=n_jobs, joblib_backend=joblib_backend)
+
+
+class MapHStack(MapStack):
+    """``MapStack(*maps, axis=1)`` (``map.py:783-825``)."""
+
+    def __init__(self, *maps, n_jobs=1, joblib_backend='loky'):
+        super().__init__(*maps, axis=1, n_jobs=n_jobs, joblib_backend=joblib_backend)
+
+
+class DiffMapStack(MapStack, DifferentiableMap):
+    """Stack of differentiable maps (``map.py:828-942``): vertical stacks have Lipschitz
+    constants ``sqrt(sum L_i^2)``, horizontal ones ``max L_i``; ``jacobianT`` is the
+    horizontal (resp. vertical) stack of the blocks' jacobianT."""
+
+    def __init__(self, *diffmaps, axis, n_jobs=1, joblib_backend='loky'):
+        MapStack.__init__(self, *diffmaps, axis=axis, n_jobs=n_jobs, joblib_backend=joblib_backend)
+        if axis == 0:
+            lip = np.sqrt(np.sum([m.lipschitz_cst ** 2 for m in self.maps]))
+            dlip = np.sqrt(np.sum([m.diff_lipschitz_cst ** 2 for m in self.maps]))
+        else:
+            lip = np.max([m.lipschitz_cst for m in self.maps])
+            dlip = np.max([m.diff_lipschitz_cst for m in self.maps])
+        DifferentiableMap.__init__(self, shape=self.shape, is_linear=self.is_linear, lipschitz_cst=lip,
+                                   diff_lipschitz_cst=dlip)
+
+    def _jacT(self, t):
+        from ..func.base import ExplicitLinearFunctional
+        from ..linop.base import LinOpHStack, LinOpVStack
+
+        def wrap(j):
+            return ExplicitLinearFunctional(j) if isinstance(j, torch.Tensor) else j
+
+        if self.axis == 0:
+            return LinOpVStack(*[wrap(m._jacT(t)) for m in self.maps], n_jobs=self.n_jobs,
+                               joblib_backend=self.joblib_backend)
+        return LinOpHStack(*[wrap(m._jacT(xi)) for m, xi in zip(self.maps, self._split(t))], n_jobs=self.n_jobs,
+                           joblib_backend=self.joblib_backend)
+
+
+class DiffMapVStack(DiffMapStack):
+    """``map.py:945-955``."""
+
+    def __init__(self, *diffmaps, n_jobs=1, joblib_backend='loky'):
+        super().__init__(*diffmaps, axis=0, n_jobs=n_jobs, joblib_backend=joblib_backend)
+
+
+class DiffMapHStack(DiffMapStack):
+    """``map.py:958-968``."""
+
+    def __init__(self, *diffmaps, n_jobs=1, joblib_backend='loky'):
+        super().__init__(*diffmaps, axis=1, n_jobs=n_jobs, joblib_backend=joblib_backend)

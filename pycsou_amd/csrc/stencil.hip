@@ -1,7 +1,8 @@
-// Finite-difference operators: FirstDerivative / Gradient / Laplacian.
+// Finite-difference operators: FirstDerivative / SecondDerivative / Gradient / Laplacian.
 //
 // Replaces the PyLops 1.x arithmetic behind pycsou/linop/diff.py:128 (FirstDerivative),
-// :882 (Gradient = VStack of FirstDerivative) and :957 (Laplacian = w0*D2_0 + w1*D2_1).
+// :218 (SecondDerivative), :882 (Gradient = VStack of FirstDerivative) and :957
+// (Laplacian = w0*D2_0 + w1*D2_1).
 // Each output element is produced by one thread; neighbour loads are coalesced along
 // the contiguous axis and re-used through L1/L2.  The per-element operation order follows
 // the NumPy slicing order of PyLops 1.x so that fp64 results agree to the last ulp or two.
@@ -131,6 +132,12 @@ __device__ __forceinline__ T d2_adj_at(const T* __restrict__ y, const Geo3& g, i
 }
 
 template <typename T>
+__global__ void k_deriv2(const T* __restrict__ x, T* __restrict__ out, Geo3 g, int a, T h2, int edge, int adj) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x)
+    out[p] = adj ? d2_adj_at(x, g, p, a, h2, edge) : d2_fwd_at(x, g, p, a, h2, edge);
+}
+
+template <typename T>
 __global__ void k_lap(const T* __restrict__ x, T* __restrict__ out, Geo3 g, T w0, T w1, T h20, T h21, int edge,
                       int adj) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x) {
@@ -171,6 +178,16 @@ static int grad(bool adj, const void* in, void* out, int ndim, const int64_t* di
 }
 
 template <typename T>
+static int deriv2(bool adj, const void* in, void* out, int ndim, const int64_t* dims, int axis, double step, int edge,
+                  hipStream_t st) {
+  Geo3 g;
+  if (!make_geo(ndim, dims, g) || axis < 0 || axis >= ndim || !in || !out) return PCS_EINVAL;
+  k_deriv2<T><<<grid_for(g.N, 256), 256, 0, st>>>((const T*)in, (T*)out, g, 3 - ndim + axis, (T)(step * step), edge,
+                                                  adj ? 1 : 0);
+  return launch_status();
+}
+
+template <typename T>
 static int lap(bool adj, const void* in, void* out, const int64_t* dims, const double* w, const double* steps, int edge,
                hipStream_t st) {
   Geo3 g;
@@ -200,6 +217,20 @@ int pcs_deriv1_adj(int dt, const void* y, void* out, int ndim, const int64_t* di
                    int edge, hipStream_t st) {
   if (dt == PCS_F32) return deriv1<float>(true, y, out, ndim, dims, axis, step, kind, edge, st);
   if (dt == PCS_F64) return deriv1<double>(true, y, out, ndim, dims, axis, step, kind, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_deriv2_fwd(int dt, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step, int edge,
+                   hipStream_t st) {
+  if (dt == PCS_F32) return deriv2<float>(false, x, out, ndim, dims, axis, step, edge, st);
+  if (dt == PCS_F64) return deriv2<double>(false, x, out, ndim, dims, axis, step, edge, st);
+  return PCS_EINVAL;
+}
+
+int pcs_deriv2_adj(int dt, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step, int edge,
+                   hipStream_t st) {
+  if (dt == PCS_F32) return deriv2<float>(true, y, out, ndim, dims, axis, step, edge, st);
+  if (dt == PCS_F64) return deriv2<double>(true, y, out, ndim, dims, axis, step, edge, st);
   return PCS_EINVAL;
 }
 

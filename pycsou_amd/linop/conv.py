@@ -113,3 +113,25 @@ class Convolve1DOp(LinearOperator):
 def Convolve1D(size, filter, reshape_dims=None, axis=0, dtype='float64', method=None):
     """``pycsou/linop/conv.py:20-164``."""
     return Convolve1DOp(size, filter, reshape_dims=reshape_dims, axis=axis, dtype=dtype, method=method)
+
+
+def _odd(n):
+    n = int(n)
+    return n + 1 if n % 2 == 0 else n
+
+
+def MovingAverage1D(window_size, shape, axis=0, dtype='float64'):
+    """``pycsou/linop/conv.py:298-359`` -> ``pylops.Smoothing1D(nsmooth, dims, dir)``: a box filter
+    ``ones(n)/n`` (an even ``n`` is raised to ``n + 1``, PyLops 1.x) applied with ``Convolve1D``
+    along ``axis``, centred (offset ``(n - 1) / 2``)."""
+    n = _odd(window_size)
+    dims = (int(shape),) if np.isscalar(shape) else tuple(int(s) for s in shape)
+    return Convolve1DOp(int(np.prod(dims)), np.ones(n) / float(n), reshape_dims=dims, axis=axis, dtype=dtype)
+
+
+def MovingAverage2D(window_shape, shape, dtype='float64'):
+    """``pycsou/linop/conv.py:362-418`` -> ``pylops.Smoothing2D(nsmooth, dims)``: the 2-D box filter
+    ``ones((n0, n1)) / (n0 n1)`` (even sizes raised to odd), centred, via ``Convolve2D``."""
+    n0, n1 = _odd(window_shape[0]), _odd(window_shape[1])
+    dims = tuple(int(s) for s in shape)
+    return Convolve2DOp(int(np.prod(dims)), np.ones((n0, n1)) / float(n0 * n1), dims, dtype=dtype)

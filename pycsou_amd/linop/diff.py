@@ -103,3 +103,101 @@ class LaplacianOp(_DiffOp):
 def Laplacian(shape, weights=(1, 1), step=1., edge=True, dtype='float64'):
     """``pycsou/linop/diff.py:885-957``."""
     return LaplacianOp(shape, weights=weights, step=step, edge=edge, dtype=dtype)
+
+
+class SecondDerivativeOp(_DiffOp):
+    """``pylops.SecondDerivative`` restated on the GPU (``pcs_deriv2_*``)."""
+
+    def __init__(self, size, shape=None, axis=0, step=1.0, edge=True, dtype='float64'):
+        dims = (size,) if shape is None else tuple(int(s) for s in shape)
+        if int(np.prod(dims)) != size:
+            raise ValueError('shape and size are not compatible')
+        if not 1 <= len(dims) <= 3:
+            raise NotImplementedError('SecondDerivative supports 1-D to 3-D arrays')
+        super().__init__((size, size), size, dtype)
+        self.dims, self.axis, self.step, self.edge = dims, int(axis), float(step), bool(edge)
+
+    def _apply(self, t):
+        return O.deriv2(t, self.dims, self.axis, self.step, self.edge)
+
+    def _adj(self, t):
+        return O.deriv2(t, self.dims, self.axis, self.step, self.edge, adjoint=True)
+
+
+def SecondDerivative(size, shape=None, axis=0, step=1.0, edge=True, dtype='float64'):
+    """``pycsou/linop/diff.py:133-219``."""
+    return SecondDerivativeOp(size, shape=shape, axis=axis, step=step, edge=edge, dtype=dtype)
+
+
+def _kill_edges(Dgen, shape, axis, order, kind):
+    from .base import DiagonalOperator
+    k = np.ones(shape=Dgen.shape[0]) if shape is None else np.ones(shape=shape)
+    if axis > 0:
+        k = np.swapaxes(k, axis, 0)
+    if kind == 'forward':
+        k[-order:] = 0
+    elif kind == 'backward':
+        k[:order] = 0
+    elif kind == 'centered':
+        k[-order:] = 0
+        k[:order] = 0
+    if axis > 0:
+        k = np.swapaxes(k, 0, axis)
+    return DiagonalOperator(k.reshape(-1)) * Dgen
+
+
+def GeneralisedDerivative(size, shape=None, axis=0, step=1.0, edge=True, dtype='float64', kind_op='iterated',
+                          kind_diff='centered', **kwargs):
+    """``pycsou/linop/diff.py:222-377``: ``D^N`` ('iterated'), ``(a^2 I - D2)^N`` ('sobolev'),
+    ``(a I + D)^N`` ('exponential') or ``P(D)`` ('polynomial'), with the unreliable edge samples
+    zeroed by a diagonal mask."""
+    from .base import IdentityOperator, PolynomialLinearOperator
+    D = FirstDerivative(size=size, shape=shape, axis=axis, step=step, edge=edge, dtype=dtype, kind=kind_diff)
+    D.is_symmetric = False
+    D2 = SecondDerivative(size=size, shape=shape, axis=axis, step=step, edge=edge, dtype=dtype)
+    if kind_op == 'iterated':
+        N = kwargs['order']
+        Dgen, order = D ** N, N
+    elif kind_op == 'sobolev':
+        I = IdentityOperator(size=size)
+        N = kwargs['order']
+        Dgen, order = ((kwargs['constant'] ** 2) * I - D2) ** N, 2 * N
+    elif kind_op == 'exponential':
+        I = IdentityOperator(size=size)
+        N = kwargs['order']
+        Dgen, order = (kwargs['constant'] * I + D) ** N, N
+    elif kind_op == 'polynomial':
+        coeffs = kwargs['coeffs']
+        Dgen, order = PolynomialLinearOperator(LinOp=D, coeffs=coeffs), len(coeffs) - 1
+    else:
+        raise NotImplementedError(
+            'Supported generalised derivative types are: iterated, sobolev, exponential, polynomial.')
+    return _kill_edges(Dgen, shape, axis, order, kind_diff)
+
+
+def GeneralisedLaplacian(shape=None, step=1., edge=True, dtype='float64', kind='iterated', **kwargs):
+    """``pycsou/linop/diff.py:960-1068``: ``Delta^N`` ('iterated'), ``(a^2 I - Delta)^N``
+    ('sobolev') or ``P(Delta)`` ('polynomial') of the 2-D ``Laplacian``, with ``order`` edge samples
+    zeroed along every axis."""
+    from .base import DiagonalOperator, IdentityOperator, PolynomialLinearOperator
+    Delta = Laplacian(shape=shape, step=step, edge=edge, dtype=dtype)
+    Delta.is_symmetric = True
+    if kind == 'iterated':
+        N = kwargs['order']
+        Dgen, order = Delta ** N, 2 * N
+    elif kind == 'sobolev':
+        I = IdentityOperator(size=shape[0] * shape[1])
+        N = kwargs['order']
+        Dgen, order = ((kwargs['constant'] ** 2) * I - Delta) ** N, 2 * N
+    elif kind == 'polynomial':
+        coeffs = kwargs['coeffs']
+        Dgen, order = PolynomialLinearOperator(LinOp=Delta, coeffs=coeffs), 2 * (len(coeffs) - 1)
+    else:
+        raise NotImplementedError('Supported generalised derivative types are: iterated, sobolev, polynomial.')
+    k = np.ones(shape=shape)
+    for ax in range(len(shape)):
+        k = np.swapaxes(k, ax, 0)
+        k[-order:] = 0
+        k[:order] = 0
+        k = np.swapaxes(k, 0, ax)
+    return DiagonalOperator(k.reshape(-1)) * Dgen

@@ -92,3 +92,33 @@ def rel(a, b):
     b = np.asarray(b, dtype=np.float64)
     nb = np.linalg.norm(b)
     return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def oracle_cps_inpaint(f, tag, dtype=np.float64):
+    """Oracle run of the notebook cell [62] golden (CPS, K = [Masking; Gradient],
+    H = L1Loss(y) (+) mu L1Norm, G = Segment(0, 1))."""
+    from oracle import pylops1 as P
+    from oracle import pycsou_ref as O
+    shape = tuple(int(s) for s in f['shape'])
+    mask, y, mu = f['mask'], f['y'].astype(dtype), float(f['mu'])
+    n = int(np.prod(shape))
+    m = int(mask.sum())
+    D = P.Gradient(shape, sampling=1., edge=True, kind='forward', dtype=dtype)
+
+    def K(x):
+        return np.concatenate([x[mask], D.matvec(x)])
+
+    def KT(z):
+        xa = np.zeros(n, dtype=dtype)
+        xa[mask] = z[:m]
+        return 0 + xa + D.rmatvec(z[m:])  # LinOpStack.adjoint: result = 0; result += ...
+
+    def hprox(v, t):  # ProxFuncHStack.prox: L1Loss = L1Norm shifted by -y (ProxFuncPreComp), mu*L1Norm
+        return np.concatenate([O.prox_l1(v[:m] + (-y), t) - (-y), O.postcomp(O.prox_l1, mu)(v[m:], t)])
+
+    p = tag + '_'
+    return O.pds(lambda x: np.zeros_like(x), lambda v, t: O.proj_segment(v, 0.0, 1.0), K, KT,
+                 lambda w, s: O.fenchel_prox(hprox, w, s), float(f[p + 'tau']), float(f[p + 'sigma']),
+                 float(f[p + 'rho']), np.zeros(n, dtype=dtype), np.zeros(m + 2 * n, dtype=dtype),
+                 max_iter=int(f[p + 'max_iter']), min_iter=int(f[p + 'min_iter']),
+                 accuracy_threshold=float(f[p + 'thr']))
