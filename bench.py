@@ -14,6 +14,13 @@ halo rows with the two neighbour ranks and all-reduces the four convergence norm
 `value` is the whole-job throughput in 4096^2-image PDS iterations per second
 (= N x slab iterations/s).
 
+Second workload in the same line (`volume_c5`, BASELINE configs[4]): the 1024^3 fp64 3-D
+TV-deconvolution (three 15-tap Convolve1D, 3-D Gradient, 0.05 L21) plane-slab sharded over
+the same N ranks (strong scaling: the whole volume at every N), PDS3DEngine with the banded
+schedule (halo exchange and sums all-gather overlapped with the interior planes).  It runs
+after the C3 measurement under a watchdog: if it fails or stalls, the C3 line is printed
+without it.
+
 Prints ONE JSON line on rank 0.
 """
 
@@ -21,6 +28,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -98,6 +106,96 @@ def cpu_baseline(n, iters):
                       f'in {dt:.1f} s on 1 host core'}
 
 
+def build_volume(n, dtype, seed=0):
+    """C5 through the public API: a piecewise-constant n^3 phantom blurred by a 15-tap
+    Gaussian (sigma 2) along each axis (Convolve1D x 3), y = h*x + 0.01 N(0,1), PDS with the
+    3-D forward Gradient and 0.05 L21Norm (isotropic TV)."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.conv import Convolve1D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    shape = (n, n, n)
+    N = n ** 3
+    xs = torch.zeros(shape, dtype=dtype, device='cuda')
+    rng = np.random.default_rng(seed)
+    for _ in range(32):
+        lo = rng.integers(0, n, 3)
+        hi = np.minimum(n, lo + rng.integers(n // 16, n // 3, 3))
+        xs[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = float(rng.uniform(0, 1))
+    r = np.arange(15) - 7
+    taps = np.exp(-0.5 * (r / 2.0) ** 2)
+    taps /= taps.sum()
+    C = None
+    for ax in range(3):
+        Ci = Convolve1D(N, taps, reshape_dims=shape, axis=ax)
+        Ci.lipschitz_cst = Ci.diff_lipschitz_cst = 1.0
+        C = Ci if C is None else Ci * C
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
+    del xs
+    K = Gradient(shape=shape, kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(3 * 4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
+    H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+               z0=torch.zeros(3 * N, dtype=dtype, device='cuda'), verbose=None)
+
+
+def volume_bench(n, dtype, K, W, world, rank):
+    """C5: the whole n^3 volume plane-slab sharded over `world` ranks; K timed iterations
+    (barrier + synchronize on both sides, max over ranks)."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    from pycsou_amd.parallel import DistComm
+    t0 = time.perf_counter()
+    pds = build_volume(n, dtype)
+    spec = pds._fused_spec()
+    assert spec is not None and spec.get('ndim') == 3, 'C5 problem must take the fused 3-D engine'
+    comm = DistComm() if world > 1 else None
+    eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, comm=comm, rank=rank,
+                      world=world, chunk=2)
+    del pds, spec
+    torch.cuda.empty_cache()
+    total = W + K + 4
+    eng.init_loop(total, total, -1.0)
+    eng.advance(W)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    eng.advance(K)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    assert eng.iterations() == W + K, (eng.iterations(), W, K)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda' if dist.get_backend() == 'nccl' else 'cpu')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt * 1e3 / K
+    elem = torch.empty(0, dtype=dtype).element_size()
+    alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
+    halo = 0 if world == 1 else (eng.hx + 3 * eng.hz) * eng.plane * elem
+    res = {'workload': f'C5 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
+                       f'(Convolve1D x3), 3-D Gradient(kind=forward), 0.05*L21Norm, PDS3DEngine, '
+                       f'{world} plane slab(s) (strong scaling: whole volume at every N)',
+           'it_per_s': round(1e3 / ms, 3), 'ms_per_iter': round(ms, 4), 'steps': K, 'warmup': W,
+           'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
+           'iteration_frac_of_hbm_peak_per_gpu': round(alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
+           'alg_bytes_per_iter': alg, 'halo_bytes_per_side_per_iter': halo,
+           'banded_overlap': bool(getattr(eng, 'banded', False) and eng.overlap),
+           'setup_s': round(t1 - t0, 1)}
+    del eng
+    if comm is not None:
+        comm.close()
+    torch.cuda.empty_cache()
+    return res
+
+
 def spin_up(eng, n_launch, min_ms=60.0):
     """Untimed, before the W warmup steps: launch the step kernel until the GPU has been busy
     for >= min_ms.  Clocks ramp over the first ~10-15 ms of sustained load (rocprofv3 traces:
@@ -159,6 +257,10 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--volume-size', type=int, default=1024, help='C5 volume edge (0: skip the volume leg)')
+    ap.add_argument('--volume-dtype', default='f64', choices=['f32', 'f64'])
+    ap.add_argument('--volume-steps', type=int, default=10)
+    ap.add_argument('--volume-timeout', type=float, default=240.0)
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
                     help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
     args = ap.parse_args()
@@ -184,6 +286,7 @@ def main():
     # iterations per chunk: the largest even divisor of both K and W (<= 50)
     chunk = max(c for c in range(2, min(K, 50) + 1, 2) if K % c == 0 and W % c == 0)
 
+    out = None
     if world > 1 or args.engine == 'slab':
         res = slab_bench(n, dtype, K, W, world)
     else:
@@ -212,6 +315,8 @@ def main():
         # figure (an event pair around each of 100 eager launches) is reported beside it
         res = {'ms_per_step': ms, 'kernel_ms': ms, 'kernel_ms_isolated': eng.time_step_kernel(min(K, 100)),
                'nblocks': eng.nblocks}
+        del eng, pds
+        torch.cuda.empty_cache()
 
     if rank == 0:
         elem = 4 if dtype == torch.float32 else 8
@@ -249,10 +354,39 @@ def main():
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:
             out['cpu_baseline'] = None
-        print(json.dumps(out))
+    if args.volume_size > 0:
+        out = volume_leg(args, out if rank == 0 else None, dtype_v=torch.float64 if args.volume_dtype == 'f64'
+                         else torch.float32, world=world, rank=rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def volume_leg(args, out, dtype_v, world, rank):
+    """Run volume_bench under a watchdog; `out` (rank 0) gains `volume_c5`.  A failure leaves
+    the C3 line as it was; a stall past --volume-timeout prints it and ends the process."""
+    def fire():
+        if out is not None:
+            out['volume_c5'] = {'error': f'no result within {args.volume_timeout:.0f} s'}
+            print(json.dumps(out), flush=True)
+        sys.stderr.write('bench: volume leg timed out\n')
+        sys.stderr.flush()
+        os._exit(0)
+    timer = threading.Timer(args.volume_timeout, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        K = max(2, args.volume_steps + args.volume_steps % 2)
+        vres = volume_bench(args.volume_size, dtype_v, K, 2, world, rank)
+    except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
+        vres = {'error': f'{type(e).__name__}: {e}'[:300]}
+        print(f'bench: volume leg failed: {vres["error"]}', file=sys.stderr)
+    timer.cancel()
+    if out is not None:
+        out['volume_c5'] = vres
+    return out
 
 
 if __name__ == '__main__':

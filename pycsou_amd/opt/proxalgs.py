@@ -212,6 +212,14 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         rows = [[i, hist[i, 0], hist[i, 1]] for i in range(n)]
         self.diagnostics = _frame(['Iter', 'Relative Improvement (primal variable)',
                                    'Relative Improvement (dual variable)'], rows)
+        if self.verbose is not None:
+            # The reference prints row ``iter`` every ``verbose`` iterations while it loops
+            # (solver.py:69-71, proxalgs.py:357-358); the fused loop never stops for the host,
+            # so the same lines are printed from the device history once the run ends.
+            for row in rows[::self.verbose]:
+                self._rows = [row]
+                self.print_diagnostics()
+            self._rows = rows
         self.converged = True
         self.iterand = {'primal_variable': self._out(x), 'dual_variable': self._out(z)}
         return self.iterand, self.converged, self.diagnostics

@@ -264,3 +264,25 @@ def test_pds3d_128_fp64_vs_oracle():
     assert rel(est['dual_variable'], z_ref) < 1e-10
     np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:],
                                np.asarray(d_ref['primal'])[1:], rtol=1e-8)
+
+
+@pytest.mark.parametrize('verbose', [1, 7])
+def test_verbose_lines_fused_match_generic(capsys, verbose):
+    """``verbose`` prints ``dict(diagnostics row)`` every ``verbose`` iterations
+    (solver.py:69-71, proxalgs.py:357-358): the fused engine prints the same lines, from its
+    device history, as the per-iteration generic path."""
+    c = pds_case('deconv2d_l21_fwd_64_psf15')
+    lines = {}
+    for eng in ('fused', 'generic'):
+        pds = build(c, np.float64, engine=eng)
+        pds.verbose = verbose
+        capsys.readouterr()
+        pds.iterate()
+        out = capsys.readouterr().out.strip().splitlines()
+        assert len(out) == len(range(0, pds.iter, verbose))
+        lines[eng] = [eval(s, {'inf': np.inf, 'np': np}) for s in out]
+    for a, b in zip(lines['fused'], lines['generic']):
+        assert list(a) == ['Iter', 'Relative Improvement (primal variable)', 'Relative Improvement (dual variable)']
+        assert a['Iter'] == b['Iter']
+        for k in list(a)[1:]:
+            assert a[k] == b[k] or abs(a[k] - b[k]) <= 1e-9 * abs(b[k]), (k, a, b)
