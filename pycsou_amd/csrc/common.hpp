@@ -39,6 +39,21 @@ __device__ __forceinline__ int row_lane_group(int l5) {
   return l5 < G ? l5 : (lane_grp(l5) == 0 ? (l5 & 3) : 4 + (l5 & 3));
 }
 
+// Workgroup barrier for LDS hand-offs only: LDS ops drained, global loads and stores left in
+// flight (__syncthreads()' release fence waits vmcnt(0)).  For kernels in which no wave reads
+// global data another wave of the launch wrote.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Buffer descriptors (hardware range check): a byte offset at or past the descriptor's size
+// reads 0 / drops the store.  Offsets are built from parts that are either valid or kOOB; with
+// every view <= 2^30 bytes a sum with any kOOB part is >= the size and two kOOB parts cannot wrap.
+constexpr uint32_t kOOB = 0x40000000u;
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc rsrc_of(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 template <typename T>
 __device__ __forceinline__ T clip1(T v) {
   // proj_linfty_ball(v, 1): y[y>1]=1; y[y<-1]=-1 (NaN passes through)

@@ -595,6 +595,246 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
   }
 }
 
+// ---- row-marching separable in-plane convolution (horizontal pass first) ----------------
+// A workgroup owns a 128-column strip of a plane and marches down a range of its rows, 16 rows
+// per step.  Each input row segment (148 columns from the aligned start of the tap window,
+// zeros outside the plane) is loaded from HBM once per strip, staged in LDS, its horizontal
+// pass (taps hb) lands in a 32-row LDS ring, and the vertical pass (taps ha) of 16 output rows
+// reads the ring: no vertical halo is recomputed (k_sep2d re-reads and re-filters 14 halo rows
+// per 32-row tile).  Work: the rows of all (plane, strip) pieces, flattened (row fastest) and
+// cut into one equal contiguous range per resident workgroup; a range that crosses into the
+// next piece restarts the march there (14 rows of prologue).  The XCD-aware block -> range map
+// keeps neighbouring strips (which share 20 halo columns) on one XCD at the same time.
+// Sums are k_sep2d's (t ascending per output): identical results for the H-first order.
+template <typename T>
+struct SepM {
+  // fp32: 32 rows per step (one step's loads must cover the HBM latency: ~19 KB per block in
+  // flight); fp64: 16 rows (LDS: 3 blocks per CU)
+  static constexpr int KT = kC1K, TX = 128, G = TX / 4, GI = G + 5, WI = 4 * GI;
+  static constexpr int RS = sizeof(T) == 4 ? 32 : 16, RING = 2 * RS, RB = RS / 8, NH = RS / 8;
+  static constexpr int NL = (RS * GI + 255) / 256;
+  static_assert(RS + KT - 1 <= RING && (RING & (RING - 1)) == 0, "ring holds the 14 rows above a step");
+  static_assert(G == 32 && (RS / RB) * G == 256, "one vertical item (RB rows) and NH horizontal rows per thread");
+};
+
+// a0 += h v0, a1 += h v1 as one packed fp32 FMA (same rounding as two v_fma_f32)
+typedef float pcs_f2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ void fma2(T& a0, T& a1, T h, T v0, T v1) {
+  const pcs_f2 a = {a0, a1}, v = {v0, v1}, hh = {h, h};
+  const pcs_f2 r = __builtin_elementwise_fma(hh, v, a);
+  a0 = r.x;
+  a1 = r.y;
+}
+
+struct SepCur {  // a step of the march: piece (plane * nstrips + strip), rows [a, b), step s of ns
+  int64_t piece;
+  int a, b, s, ns;
+};
+
+template <typename T, int SHIFT, bool VEC>
+__global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T* __restrict__ out, int n1, int n2,
+                                                     int nstrips, int64_t total, const T* __restrict__ ha_, int ka,
+                                                     int offa, const T* __restrict__ hb_, int kb, int S0) {
+  using S = SepM<T>;
+  constexpr int KT = S::KT, TX = S::TX, GI = S::GI, WI = S::WI, RS = S::RS, RING = S::RING, RB = S::RB, NL = S::NL,
+                NH = S::NH;
+  constexpr int NW = (SHIFT + KT + 3 + 3) / 4;  // Q4 slots of one horizontal window
+  __shared__ __attribute__((aligned(16))) T stg[RS * WI];
+  __shared__ __attribute__((aligned(16))) T ring[RING * TX];
+  T ha[KT], hb[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    ha[t] = t < ka ? ha_[t] : T(0);
+    hb[t] = t < kb ? hb_[t] : T(0);
+  }
+  // XCD-aware bijective block -> range map: the blocks of XCD (b % 8) take consecutive ranges
+  int64_t task;
+  {
+    const int64_t b = blockIdx.x, nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = b % 8, k = b / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int64_t R0 = task * total / gridDim.x, R1 = (task + 1) * total / gridDim.x;
+  if (R0 >= R1) return;
+  const int tid = threadIdx.x, g = tid & 31, hrow = tid >> 5;
+  auto piece_at = [&](int64_t r) {  // the step cursor at flattened row r (< R1)
+    SepCur c;
+    c.piece = r / n1;
+    c.a = (int)(r - c.piece * n1);
+    const int64_t end = (c.piece + 1) * n1 < R1 ? (c.piece + 1) * n1 : R1;
+    c.b = (int)(end - c.piece * n1);
+    c.s = 0;
+    c.ns = (c.b - c.a + KT - 1 + RS - 1) / RS;
+    return c;
+  };
+  Q4<T> q[NL];
+  // loads of step c: input rows k = s RS + rr (global row a + offa - 14 + k) of the piece
+  auto prefetch = [&](const SepCur& c) {
+    const int64_t pl = c.piece / nstrips;
+    const int j0 = (int)(c.piece - pl * nstrips) * TX;
+    const T* src = in + pl * (int64_t)n1 * n2;
+    const int kmax = c.b - c.a + KT - 2;  // last input row any output of [a, b) reads
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = min(l * 256 + tid, RS * GI - 1);
+      const int rr = e / GI, qq = e - (e / GI) * GI;
+      const int k = c.s * RS + rr, gi = c.a + offa - (KT - 1) + k, gc = j0 + S0 + 4 * qq;
+      const bool rin = gi >= 0 && gi < n1 && k <= kmax;
+      if (VEC) {
+        const bool ok = rin && gc >= 0 && gc + 4 <= n2;
+        const Q4<T> v = ldq(src + (ok ? (int64_t)gi * n2 + gc : 0));
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
+      } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const bool ok = rin && gc + m >= 0 && gc + m < n2;
+          const T v = src[ok ? (int64_t)gi * n2 + gc + m : 0];
+          q[l].v[m] = ok ? v : T(0);
+        }
+      }
+    }
+  };
+  SepCur cur = piece_at(R0);
+  prefetch(cur);
+  for (;;) {
+    // staging <- the landed rows of this step (slot e = row * GI + group: pitch WI)
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = l * 256 + tid;
+      if (e < RS * GI) stq(stg + 4 * e, q[l]);
+    }
+    lds_barrier();  // staging landed; the previous step's vertical pass is done with the ring
+    SepCur nxt = cur;
+    bool more = true;
+    if (cur.s + 1 < cur.ns) {
+      nxt.s = cur.s + 1;
+    } else {
+      const int64_t done = cur.piece * n1 + cur.b;
+      more = done < R1;
+      if (more) nxt = piece_at(done);
+    }
+    if (more) prefetch(nxt);
+    // horizontal pass: rows hrow + 8 h of the step, output group g -> ring slot of row k
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int i = hrow + 8 * h;
+      T w[NW * 4];
+#pragma unroll
+      for (int u = 0; u < NW; ++u) {
+        const Q4<T> v = ldsq(stg + i * WI + 4 * (g + u));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[4 * u + e] = v.v[e];
+      }
+      Q4<T> o;
+      if constexpr (sizeof(T) == 4) {  // columns (0, 1) and (2, 3) as packed pairs
+#pragma unroll
+        for (int m = 0; m < 4; m += 2) {
+          T a0 = T(0), a1 = T(0);
+#pragma unroll
+          for (int t = 0; t < KT; ++t) fma2(a0, a1, hb[t], w[SHIFT + m + (KT - 1 - t)], w[SHIFT + m + 1 + (KT - 1 - t)]);
+          o.v[m] = a0;
+          o.v[m + 1] = a1;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          T acc = T(0);
+#pragma unroll
+          for (int t = 0; t < KT; ++t) acc += hb[t] * w[SHIFT + m + (KT - 1 - t)];
+          o.v[m] = acc;
+        }
+      }
+      stq(ring + ((cur.s * RS + i) & (RING - 1)) * TX + 4 * g, o);
+    }
+    lds_barrier();
+    // vertical pass: output rows a - 14 + s RS + 2 hrow + r read ring rows k - 14 .. k
+    {
+      const int r0 = RB * hrow, kb0 = cur.s * RS + r0 - (KT - 1);
+      Q4<T> acc[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
+#pragma unroll
+      for (int j = RB + KT - 2; j >= 0; --j) {
+        const Q4<T> v = ldsq(ring + ((kb0 + j) & (RING - 1)) * TX + 4 * g);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int t = r + KT - 1 - j;
+          if (t >= 0 && t < KT) {
+            if constexpr (sizeof(T) == 4) {  // v_pk_fma_f32: two columns per instruction
+              fma2(acc[r].v[0], acc[r].v[1], ha[t], v.v[0], v.v[1]);
+              fma2(acc[r].v[2], acc[r].v[3], ha[t], v.v[2], v.v[3]);
+            } else {
+#pragma unroll
+              for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
+            }
+          }
+        }
+      }
+      const int64_t pl = cur.piece / nstrips;
+      const int gc = (int)(cur.piece - pl * nstrips) * TX + 4 * g;
+      T* dst = out + pl * (int64_t)n1 * n2;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int o = cur.a - (KT - 1) + cur.s * RS + r0 + r;
+        if (o < cur.a || o >= cur.b) continue;
+        if (VEC) {
+          if (gc < n2) stq(dst + (int64_t)o * n2 + gc, acc[r]);
+        } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (gc + m < n2) dst[(int64_t)o * n2 + gc + m] = acc[r].v[m];
+        }
+      }
+    }
+    if (!more) break;
+    cur = nxt;
+  }
+}
+
+// resident workgroups of k_sep2d_march<T> on the device (queried once per type)
+template <typename T>
+static int sep_march_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_march<T, 0, true>, 256, 0) != hipSuccess || nb < 1)
+      nb = 2;
+    (void)hipGetLastError();
+    slots = cus * nb;
+  }
+  return slots;
+}
+
+template <typename T>
+static void launch_sep2d_march(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka,
+                               int offa, const void* hb, int kb, int offb, hipStream_t st) {
+  using S = SepM<T>;
+  const int64_t nstrips = (n2 + S::TX - 1) / S::TX, total = np * nstrips * n1;
+  const int d = offb - (S::KT - 1);  // first tap-window column relative to the output column
+  const int S0 = d >= 0 ? 0 : -((-d + 3) / 4) * 4, shift = d - S0;
+  int64_t grid = sep_march_slots<T>();
+  const int64_t by_rows = (total + 63) / 64;  // ranges of at least 64 rows
+  grid = grid < by_rows ? grid : by_rows;
+  grid = grid < 1 ? 1 : grid;
+  auto args = [&](auto kern) {
+    kern<<<(unsigned)grid, 256, 0, st>>>((const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, total, (const T*)ha,
+                                         ka, offa, (const T*)hb, kb, S0);
+  };
+  const bool vec = n2 % 4 == 0;
+  switch (shift) {
+    case 0: vec ? args(k_sep2d_march<T, 0, true>) : args(k_sep2d_march<T, 0, false>); break;
+    case 1: vec ? args(k_sep2d_march<T, 1, true>) : args(k_sep2d_march<T, 1, false>); break;
+    case 2: vec ? args(k_sep2d_march<T, 2, true>) : args(k_sep2d_march<T, 2, false>); break;
+    default: vec ? args(k_sep2d_march<T, 3, true>) : args(k_sep2d_march<T, 3, false>); break;
+  }
+}
+
 template <typename T, bool VFIRST>
 static void launch_sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
                          const void* hb, int kb, int offb, hipStream_t st) {
@@ -638,8 +878,15 @@ static int sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, 
   if ((uintptr_t)in % 16 || (uintptr_t)out % 16) return PCS_EINVAL;
   if (np == 0) return PCS_OK;
   if (np * ((n1 + S::TY - 1) / S::TY) * ((n2 + S::TX - 1) / S::TX) >= (1LL << 31)) return PCS_EUNSUPPORTED;
+  static int mode = -1;  // PCS_SEP2D_TILE=1: the tile kernel for the H-first order (diagnostics)
+  if (mode < 0) {
+    const char* e = getenv("PCS_SEP2D_TILE");
+    mode = (e && e[0] == '1') ? 1 : 0;
+  }
   if (vfirst)
     launch_sep2d<T, true>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
+  else if (mode == 0 && n1 < (1LL << 30) && n2 < (1LL << 30))
+    launch_sep2d_march<T>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
   else
     launch_sep2d<T, false>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
   return launch_status();

@@ -81,10 +81,6 @@ __device__ __forceinline__ unsigned long long pcs_stamp() {
   } while (0)
 #endif
 
-// Workgroup barrier for LDS hand-offs only: LDS ops drained, global loads and stores left in
-// flight (__syncthreads()' release fence waits vmcnt(0)).  No wave of this kernel reads
-// global data another wave of the launch wrote.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Own-row bands of one launch: segments [ra0, rb0) first (nseg0 of them), then [ra1, rb1).
 // The whole slab is {seg_len, nseg, 0, rows, rows, rows}; the multi-GPU loop launches the
@@ -120,12 +116,6 @@ __device__ __forceinline__ float to_vgpr(float v) {
 // slab and columns outside [0, n1) cost no branch and no select -- their offset carries kOOB.
 // Each part (row, column) is either valid or kOOB; with every view <= 2^30 bytes a sum with
 // any kOOB part is >= the size and two kOOB parts (2^31) cannot wrap.
-constexpr uint32_t kOOB = 0x40000000u;
-typedef __amdgpu_buffer_rsrc_t Rsrc;
-
-__device__ __forceinline__ Rsrc rsrc_of(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
 __device__ __forceinline__ G4<float> bload4(Rsrc r, uint32_t off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return {{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])}};

@@ -308,3 +308,27 @@ def test_lipschitz_lanczos(A):
     C.compute_lipschitz_cst()
     dense = np.stack([P.Convolve2D(4096, h, (64, 64), offset=(3, 3)).matvec(e) for e in np.eye(4096)[:: 1]]).T
     assert abs(C.lipschitz_cst - np.linalg.norm(dense, 2)) < 1e-6
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('ka,offa,kb,offb', [(15, 7, 15, 7), (15, 14, 15, 0), (6, 2, 9, 8)])
+@pytest.mark.parametrize('dims', [(4, 200, 264), (2, 1100, 128), (9, 17, 36), (3, 150, 131), (40, 64, 256)])
+def test_conv2d_sep_planes_march(A, dtype, ka, offa, kb, offb, dims):
+    """The row-marching H-first kernel (ranges crossing planes and strips, ragged last strip,
+    odd widths) == pcs_conv1d along axis 2 then axis 1 (same tap order; the rounding of the
+    contiguous-axis kernel differs by an ulp here and there)."""
+    from pycsou_amd import _lib as L
+    rng = np.random.default_rng(ka * 7 + kb + dims[2])
+    x = dev(rng.standard_normal(dims).astype(dtype))
+    ha, hb = dev(rng.standard_normal(ka).astype(dtype)), dev(rng.standard_normal(kb).astype(dtype))
+    lib, st = L.load(), L.stream()
+    t1, ref = torch.empty_like(x), torch.empty_like(x)
+    out = torch.full_like(x, float('nan'))
+    d = L.i64s(dims)
+    assert lib.pcs_conv1d(L.dtcode(x), L.ptr(x), L.ptr(t1), 3, d, 2, L.ptr(hb), kb, offb, st) == 0
+    assert lib.pcs_conv1d(L.dtcode(x), L.ptr(t1), L.ptr(ref), 3, d, 1, L.ptr(ha), ka, offa, st) == 0
+    assert lib.pcs_conv2d_sep_planes(L.dtcode(x), L.ptr(x), L.ptr(out), dims[0], dims[1], dims[2], L.ptr(ha), ka,
+                                     offa, L.ptr(hb), kb, offb, 0, st) == 0
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()  # every output written
+    assert rel(host(out), host(ref)) < TOL[dtype]
