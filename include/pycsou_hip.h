@@ -156,6 +156,18 @@ int64_t pcs_reduce_ws_bytes(void);
 int pcs_reduce(int dtype, int kind, const void* x, const void* y, int64_t n, double* out_dev, void* ws,
                hipStream_t stream);
 
+/* One fused AcceleratedProximalGradientDescent.update_iterand + update_diagnostics
+ * (pycsou/opt/proxalgs.py:586-601 and 612-622), given g = grad F(x):
+ *   x_t = G.prox(x - tau g, tau)   gkind PCS_G_NULL / PCS_G_NONNEG / PCS_G_SEGMENT [seg_a, seg_b] /
+ *                                  PCS_APGD_G_L1 (lam * L1Norm: soft threshold tau*lam)
+ *   x'  = x_t + a (x_t - aux)      aux = the previous x_t ('past_aux'), a = (t_old - 1) / t
+ * writes x' -> xn, x_t -> aux_n (no aliasing) and sums_dev[0..1] = ||x - x'||^2, ||x||^2 (fp64,
+ * fixed order).  ws >= pcs_reduce_ws_bytes(). */
+enum { PCS_APGD_G_L1 = 3 };
+int pcs_apgd_step(int dtype, const void* x, const void* g, const void* aux, void* xn, void* aux_n, int64_t n,
+                  double tau, double a, int gkind, double lam, double seg_a, double seg_b, double* sums_dev,
+                  void* ws, hipStream_t stream);
+
 /* ---------------------------------------------------------------- fused PDS iteration */
 
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics
@@ -234,6 +246,11 @@ typedef struct {
   void* recv_hi[4];
   int64_t bytes[4];
 } pcs_halo_set;
+
+/* One grouped RCCL send/recv of the halo rows/planes with the two neighbour ranks on `stream`
+ * (the exchange step of SURVEY 8(e)): send_lo -> rank-1's recv_hi, send_hi -> rank+1's recv_lo.
+ * world == 1: no-op.  Graph-capturable (no allocation, no host synchronisation). */
+int pcs_halo_exchange(void* comm, int rank, int world, const pcs_halo_set* h, hipStream_t stream);
 
 typedef struct {
   int world, rank;

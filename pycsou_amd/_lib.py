@@ -18,6 +18,7 @@ PCS_F32, PCS_F64 = 0, 1
 PCS_FORWARD, PCS_BACKWARD, PCS_CENTERED = 0, 1, 2
 PCS_H_L1, PCS_H_L21 = 0, 1
 PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
+PCS_APGD_G_L1 = 3
 PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF = 0, 1, 2, 3
 KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
 
@@ -94,6 +95,8 @@ _SIGS = {
     'pcs_sub2': (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
     'pcs_reduce_ws_bytes': (_c_i64, []),
     'pcs_reduce': (_c_int, [_c_int, _c_int, _vp, _vp, _c_i64, _vp, _vp, _vp]),
+    'pcs_apgd_step': (_c_int, [_c_int, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _c_int, _c_dbl, _c_dbl,
+                                _c_dbl, _vp, _vp, _vp]),
     'pcs_pds2d_halo_x': (_c_int, [_c_int]),
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
@@ -106,6 +109,7 @@ _SIGS = {
     'pcs_comm_unique_id': (_c_int, [_vp]),
     'pcs_comm_init': (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(_vp)]),
     'pcs_comm_destroy': (_c_int, [_vp]),
+    'pcs_halo_exchange': (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(HaloSet), _vp]),
     'pcs_slab2d_create': (_c_int, [ctypes.POINTER(Slab2DDesc), _vp, ctypes.POINTER(_vp)]),
     'pcs_slab2d_overlapped': (_c_int, [_vp]),
     'pcs_slab2d_run': (_c_int, [_vp, _c_i64, _c_int, _vp]),

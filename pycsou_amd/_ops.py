@@ -118,6 +118,18 @@ def reduce_dev(kind, x, y=None, out=None):
     return out
 
 
+def apgd_step(x, g, aux, tau, a, gkind, lam=1.0, seg=(0.0, 1.0), sums=None):
+    """Fused APGD update (``pcs_apgd_step``): returns (x', x_t, sums) with sums[0..1] =
+    ||x - x'||^2, ||x||^2 on the device."""
+    lib = L.gpu()
+    xn, auxn = torch.empty_like(x), torch.empty_like(x)
+    sums = torch.empty(2, dtype=torch.float64, device=x.device) if sums is None else sums
+    L.check(lib.pcs_apgd_step(L.dtcode(x), L.ptr(x), L.ptr(g), L.ptr(aux), L.ptr(xn), L.ptr(auxn), x.numel(),
+                              float(tau), float(a), int(gkind), float(lam), float(seg[0]), float(seg[1]), L.ptr(sums),
+                              L.ptr(_ws(x)), L.stream()), 'pcs_apgd_step')
+    return xn, auxn, sums
+
+
 def sumsq(x):
     return float(reduce_dev(0, x).item())
 

@@ -617,16 +617,6 @@ struct SepM {
   static_assert(G == 32 && (RS / RB) * G == 256, "one vertical item (RB rows) and NH horizontal rows per thread");
 };
 
-// a0 += h v0, a1 += h v1 as one packed fp32 FMA (same rounding as two v_fma_f32)
-typedef float pcs_f2 __attribute__((ext_vector_type(2)));
-template <typename T>
-__device__ __forceinline__ void fma2(T& a0, T& a1, T h, T v0, T v1) {
-  const pcs_f2 a = {a0, a1}, v = {v0, v1}, hh = {h, h};
-  const pcs_f2 r = __builtin_elementwise_fma(hh, v, a);
-  a0 = r.x;
-  a1 = r.y;
-}
-
 struct SepCur {  // a step of the march: piece (plane * nstrips + strip), rows [a, b), step s of ns
   int64_t piece;
   int a, b, s, ns;
@@ -727,23 +717,12 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
         for (int e = 0; e < 4; ++e) w[4 * u + e] = v.v[e];
       }
       Q4<T> o;
-      if constexpr (sizeof(T) == 4) {  // columns (0, 1) and (2, 3) as packed pairs
 #pragma unroll
-        for (int m = 0; m < 4; m += 2) {
-          T a0 = T(0), a1 = T(0);
+      for (int m = 0; m < 4; ++m) {
+        T acc = T(0);
 #pragma unroll
-          for (int t = 0; t < KT; ++t) fma2(a0, a1, hb[t], w[SHIFT + m + (KT - 1 - t)], w[SHIFT + m + 1 + (KT - 1 - t)]);
-          o.v[m] = a0;
-          o.v[m + 1] = a1;
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          T acc = T(0);
-#pragma unroll
-          for (int t = 0; t < KT; ++t) acc += hb[t] * w[SHIFT + m + (KT - 1 - t)];
-          o.v[m] = acc;
-        }
+        for (int t = 0; t < KT; ++t) acc += hb[t] * w[SHIFT + m + (KT - 1 - t)];
+        o.v[m] = acc;
       }
       stq(ring + ((cur.s * RS + i) & (RING - 1)) * TX + 4 * g, o);
     }
@@ -763,13 +742,8 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
         for (int r = 0; r < RB; ++r) {
           const int t = r + KT - 1 - j;
           if (t >= 0 && t < KT) {
-            if constexpr (sizeof(T) == 4) {  // v_pk_fma_f32: two columns per instruction
-              fma2(acc[r].v[0], acc[r].v[1], ha[t], v.v[0], v.v[1]);
-              fma2(acc[r].v[2], acc[r].v[3], ha[t], v.v[2], v.v[3]);
-            } else {
 #pragma unroll
-              for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
-            }
+            for (int m = 0; m < 4; ++m) acc[r].v[m] += ha[t] * v.v[m];
           }
         }
       }

@@ -175,6 +175,57 @@ static int reduce(int kind, const void* x, const void* y, int64_t n, double* out
   return launch_status();
 }
 
+// One fused AcceleratedProximalGradientDescent.update_iterand + update_diagnostics
+// (pycsou/opt/proxalgs.py:586-601, 612-622) given g = grad F(x) (computed by F's operators):
+//   x_t = G.prox(x - tau g, tau)        G: null / NonNegativeOrthant / Segment / lam*L1Norm
+//   x'  = x_t + a (x_t - aux)           aux = previous x_t ('past_aux'), a = (t_old - 1) / t
+// plus per-block partials of ||x - x'||^2 and ||x||^2 (stage 2: k_apgd_sums, fixed order).
+template <typename T>
+__global__ __launch_bounds__(256) void k_apgd_step(const T* __restrict__ x, const T* __restrict__ g,
+                                                   const T* __restrict__ aux, T* __restrict__ xn, T* __restrict__ auxn,
+                                                   int64_t n, T tau, T a, int gk, T thr, T sa, T sb,
+                                                   double* __restrict__ part) {
+  __shared__ double sm[8];
+  double v[2] = {0.0, 0.0};
+  PCS_GRID_LOOP(p, n) {
+    const T xv = x[p];
+    T w = xv - tau * g[p];
+    if (gk == PCS_APGD_G_L1) {
+      w = prox_l1_el(w, thr);  // lam*L1: prox(x, tau*lam)  (functional.py:264-265, base.py:239-240)
+    } else if (gk == PCS_G_NONNEG) {
+      w = (w < T(0)) ? T(0) : w;  // math/prox.py:295-297
+    } else if (gk == PCS_G_SEGMENT) {
+      w = (w < sa) ? sa : w;  // math/prox.py:340-343
+      w = (w > sb) ? sb : w;
+    }
+    const T xnew = w + a * (w - aux[p]);
+    auxn[p] = w;
+    xn[p] = xnew;
+    const double d = (double)xv - (double)xnew;
+    v[0] += d * d;
+    v[1] += (double)xv * (double)xv;
+  }
+  block_sum<2>(v, sm);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = v[0];
+    part[2 * blockIdx.x + 1] = v[1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_apgd_sums(const double* __restrict__ part, int np, double* __restrict__ out) {
+  __shared__ double sm[8];
+  double v[2] = {0.0, 0.0};
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    v[0] += part[2 * i];
+    v[1] += part[2 * i + 1];
+  }
+  block_sum<2>(v, sm);
+  if (threadIdx.x == 0) {
+    out[0] = v[0];
+    out[1] = v[1];
+  }
+}
+
 }  // namespace pcs
 
 using namespace pcs;
@@ -271,7 +322,23 @@ int pcs_sub2(int dt, const void* x, const void* y, const void* w, void* out, int
   return launch_status();
 }
 
-int64_t pcs_reduce_ws_bytes(void) { return (int64_t)sizeof(double) * kRedBlocks; }
+int64_t pcs_reduce_ws_bytes(void) { return (int64_t)sizeof(double) * 2 * kRedBlocks; }
+
+int pcs_apgd_step(int dt, const void* x, const void* g, const void* aux, void* xn, void* aux_n, int64_t n, double tau,
+                  double a, int gkind, double lam, double seg_a, double seg_b, double* sums_dev, void* ws,
+                  hipStream_t st) {
+  if (!x || !g || !aux || !xn || !aux_n || !sums_dev || !ws || n < 0) return PCS_EINVAL;
+  if (gkind != PCS_G_NULL && gkind != PCS_G_NONNEG && gkind != PCS_G_SEGMENT && gkind != PCS_APGD_G_L1)
+    return PCS_EINVAL;
+  if (xn == x || xn == aux || aux_n == x || aux_n == aux || xn == aux_n) return PCS_EINVAL;
+  if (gkind == PCS_APGD_G_L1 && !(tau * lam > 0)) return PCS_EINVAL;
+  const unsigned gr = grid_for(n, 256, kRedBlocks);
+  PCS_DISPATCH(dt, k_apgd_step<T><<<gr, 256, 0, st>>>((const T*)x, (const T*)g, (const T*)aux, (T*)xn, (T*)aux_n, n,
+                                                       (T)tau, (T)a, gkind, (T)(tau * lam), (T)seg_a, (T)seg_b,
+                                                       (double*)ws));
+  k_apgd_sums<<<1, 256, 0, st>>>((const double*)ws, (int)gr, sums_dev);
+  return launch_status();
+}
 
 int pcs_reduce(int dt, int kind, const void* x, const void* y, int64_t n, double* out, void* ws, hipStream_t st) {
   if (dt == PCS_F32) return reduce<float>(kind, x, y, n, out, ws, st);

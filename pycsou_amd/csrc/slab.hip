@@ -78,26 +78,41 @@ struct Slab2DPlan {
   bool overlap;
 };
 
-static int halo_exchange(const Slab2DPlan& P, const pcs_halo_set& h, hipStream_t st) {
+static int halo_exchange_on(ncclComm_t comm, int rank, int world, const pcs_halo_set& h, hipStream_t st) {
   const Rccl& R = rccl();
-  const int lo = P.d.rank - 1, hi = P.d.rank + 1;
-  const bool has_lo = lo >= 0, has_hi = hi < P.d.world;
+  const int lo = rank - 1, hi = rank + 1;
+  const bool has_lo = lo >= 0, has_hi = hi < world;
   if (!has_lo && !has_hi) return PCS_OK;
   if (R.group_start() != ncclSuccess) return PCS_ELAUNCH;
   int bad = 0;
   for (int k = 0; k < h.nbuf; ++k) {
     const size_t nb = (size_t)h.bytes[k];
     if (has_lo) {
-      bad |= R.send(h.send_lo[k], nb, ncclUint8, lo, P.comm, st) != ncclSuccess;
-      bad |= R.recv(h.recv_lo[k], nb, ncclUint8, lo, P.comm, st) != ncclSuccess;
+      bad |= R.send(h.send_lo[k], nb, ncclUint8, lo, comm, st) != ncclSuccess;
+      bad |= R.recv(h.recv_lo[k], nb, ncclUint8, lo, comm, st) != ncclSuccess;
     }
     if (has_hi) {
-      bad |= R.send(h.send_hi[k], nb, ncclUint8, hi, P.comm, st) != ncclSuccess;
-      bad |= R.recv(h.recv_hi[k], nb, ncclUint8, hi, P.comm, st) != ncclSuccess;
+      bad |= R.send(h.send_hi[k], nb, ncclUint8, hi, comm, st) != ncclSuccess;
+      bad |= R.recv(h.recv_hi[k], nb, ncclUint8, hi, comm, st) != ncclSuccess;
     }
   }
   bad |= R.group_end() != ncclSuccess;
   return bad ? PCS_ELAUNCH : PCS_OK;
+}
+
+static int halo_exchange(const Slab2DPlan& P, const pcs_halo_set& h, hipStream_t st) {
+  return halo_exchange_on(P.comm, P.d.rank, P.d.world, h, st);
+}
+
+// argument checks shared by pcs_slab2d_create and pcs_halo_exchange
+static bool halo_set_ok(const pcs_halo_set& h, int rank, int world) {
+  if (h.nbuf < 0 || h.nbuf > 4) return false;
+  for (int k = 0; k < h.nbuf; ++k) {
+    if (h.bytes[k] < 0) return false;
+    if (rank > 0 && (!h.send_lo[k] || !h.recv_lo[k])) return false;
+    if (rank < world - 1 && (!h.send_hi[k] || !h.recv_hi[k])) return false;
+  }
+  return true;
 }
 
 // all-gather of this rank's 4 sums (parity q) + the loop control over the gathered sums
@@ -214,15 +229,8 @@ int pcs_comm_destroy(void* comm) {
 int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan) {
   if (!d || !plan || d->world < 1 || d->rank < 0 || d->rank >= d->world || !d->ctrl || !d->hist) return PCS_EINVAL;
   if (d->world > 1 && (!comm || !rccl().ok)) return PCS_EINVAL;
-  for (int p = 0; p < 2; ++p) {
-    const pcs_halo_set& h = d->halo[p];
-    if (h.nbuf < 0 || h.nbuf > 4) return PCS_EINVAL;
-    for (int k = 0; k < h.nbuf; ++k) {
-      if (h.bytes[k] < 0) return PCS_EINVAL;
-      if (d->rank > 0 && (!h.send_lo[k] || !h.recv_lo[k])) return PCS_EINVAL;
-      if (d->rank < d->world - 1 && (!h.send_hi[k] || !h.recv_hi[k])) return PCS_EINVAL;
-    }
-  }
+  for (int p = 0; p < 2; ++p)
+    if (!halo_set_ok(d->halo[p], d->rank, d->world)) return PCS_EINVAL;
   Slab2DPlan* P = new (std::nothrow) Slab2DPlan();
   if (!P) return PCS_ELAUNCH;
   P->d = *d;
@@ -254,6 +262,13 @@ int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan) {
   }
   *plan = P;
   return PCS_OK;
+}
+
+int pcs_halo_exchange(void* comm, int rank, int world, const pcs_halo_set* h, hipStream_t st) {
+  if (!h || world < 1 || rank < 0 || rank >= world || !halo_set_ok(*h, rank, world)) return PCS_EINVAL;
+  if (world == 1) return PCS_OK;
+  if (!comm || !rccl().ok) return PCS_EINVAL;
+  return halo_exchange_on((ncclComm_t)comm, rank, world, *h, st);
 }
 
 int pcs_slab2d_overlapped(const void* plan) { return plan && ((const Slab2DPlan*)plan)->overlap ? 1 : 0; }

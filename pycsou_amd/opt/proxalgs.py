@@ -370,17 +370,46 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         self.iterand = {'iterand': self._out(x), 'past_aux': self._out(aux), 'past_t': t}
         return self.iterand, self.converged, self.diagnostics
 
-    def _update_dev(self, st):
-        """``proxalgs.py:586-601``."""
-        x, x_old, t_old = st
-        x_temp = self.G._prox(O.axpby(x, self.F._grad(x), 1.0, -self.tau), self.tau)
+    def _g_kind(self):
+        """(kind, lam, seg) of G for the fused step (pcs_apgd_step), or None."""
+        from .. import _lib as L
+        from ..core.functional import ProxFuncPostComp
+        from ..func.base import IndicatorFunctional
+        from ..func.penalty import L1Norm
+        G, lam = self.G, 1.0
+        if isinstance(G, ProxFuncPostComp) and G.shift == 0 and isinstance(G.prox_func, L1Norm):
+            G, lam = G.prox_func, float(G.scale)
+        if isinstance(G, NullProximableFunctional):
+            return L.PCS_G_NULL, 1.0, (0.0, 1.0)
+        if isinstance(G, L1Norm):
+            return L.PCS_APGD_G_L1, lam, (0.0, 1.0)
+        if isinstance(G, IndicatorFunctional) and G.kind == 'nonneg':
+            return L.PCS_G_NONNEG, 1.0, (0.0, 1.0)
+        if isinstance(G, IndicatorFunctional) and G.kind == 'segment':
+            return L.PCS_G_SEGMENT, 1.0, tuple(G.params)
+        return None
+
+    def _momentum(self, t_old):
         if self.acceleration == 'BT':
             t = (1 + np.sqrt(1 + 4 * t_old ** 2)) / 2
         elif self.acceleration == 'CD':
             t = (self.iter + self.d) / self.d
         else:
             t = t_old = 1
-        a = (t_old - 1) / t
+        return t, (t_old - 1) / t
+
+    def _update_dev(self, st):
+        """``proxalgs.py:586-601``: G.prox, the momentum step and the diagnostics' two norms in
+        one kernel (pcs_apgd_step) when G is null / lam*L1 / an orthant or segment indicator."""
+        x, x_old, t_old = st
+        t, a = self._momentum(t_old)
+        gk = self._g_kind()
+        if gk is not None:
+            kind, lam, seg = gk
+            xn, x_temp, self._sums = O.apgd_step(x, self.F._grad(x), x_old, self.tau, a, kind, lam, seg)
+            return (xn, x_temp, t)
+        self._sums = None
+        x_temp = self.G._prox(O.axpby(x, self.F._grad(x), 1.0, -self.tau), self.tau)
         x = O.axpby(x_temp, O.axpby(x_temp, x_old, 1.0, -1.0), 1.0, a)
         return (x, x_temp, t)
 
@@ -401,7 +430,12 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         return self._rows[self.iter - 1][1]
 
     def update_diagnostics(self):
-        self._rows.append([self.iter, _rel_improvement(self._old, self._state[0])])
+        sums = getattr(self, '_sums', None)
+        if sums is None:
+            self._rows.append([self.iter, _rel_improvement(self._old, self._state[0])])
+            return
+        d2, n2 = sums.tolist()  # ||x_old - x||^2, ||x_old||^2 from the fused step
+        self._rows.append([self.iter, np.inf if n2 == 0 else float(np.sqrt(d2) / np.sqrt(n2))])
 
 
 APGD = AcceleratedProximalGradientDescent

@@ -332,3 +332,35 @@ def test_conv2d_sep_planes_march(A, dtype, ka, offa, kb, offb, dims):
     torch.cuda.synchronize()
     assert not torch.isnan(out).any()  # every output written
     assert rel(host(out), host(ref)) < TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('gkind', ['null', 'l1', 'nonneg', 'segment'])
+@pytest.mark.parametrize('n', [1, 1000, 300001])
+def test_apgd_step(A, dtype, gkind, n):
+    """pcs_apgd_step == the reference update (proxalgs.py:586-601) restated in NumPy:
+    x_t = G.prox(x - tau g, tau), x' = x_t + a (x_t - aux), and the two diagnostics norms."""
+    from oracle import pycsou_ref as OR
+    from pycsou_amd import _lib as L
+    _, O = A
+    rng = np.random.default_rng(n)
+    x, g, aux = (rng.standard_normal(n).astype(dtype) for _ in range(3))
+    tau, a, lam, seg = 0.37, 0.61, 0.8, (-0.25, 0.5)
+    v = x.astype(np.float64) - tau * g.astype(np.float64)
+    if gkind == 'l1':
+        xt = OR.prox_l1(v, tau * lam)
+    elif gkind == 'nonneg':
+        xt = np.maximum(v, 0)
+    elif gkind == 'segment':
+        xt = np.clip(v, *seg)
+    else:
+        xt = v
+    xn_ref = xt + a * (xt - aux)
+    kind = {'null': L.PCS_G_NULL, 'l1': L.PCS_APGD_G_L1, 'nonneg': L.PCS_G_NONNEG, 'segment': L.PCS_G_SEGMENT}[gkind]
+    xn, xtd, sums = O.apgd_step(dev(x), dev(g), dev(aux), tau, a, kind, lam, seg)
+    tol = 10 * TOL[dtype]
+    assert rel(host(xtd), xt) < tol and rel(host(xn), xn_ref) < tol
+    d2, n2 = host(sums)
+    xn_h = host(xn).astype(np.float64)
+    assert abs(d2 - np.sum((x.astype(np.float64) - xn_h) ** 2)) <= 1e-9 * max(1.0, d2)
+    assert abs(n2 - np.sum(x.astype(np.float64) ** 2)) <= 1e-9 * n2

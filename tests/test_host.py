@@ -103,3 +103,19 @@ def test_graft_entry_importable():
     import importlib
     m = importlib.import_module('__graft_entry__')
     assert callable(m.build) and callable(m.smoke)
+
+
+def test_halo_exchange_argument_checks():
+    """pcs_halo_exchange validates on the host before touching RCCL: bad rank/world or missing
+    neighbour buffers -> PCS_EINVAL; world 1 -> no-op."""
+    import ctypes
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    h = _lib.HaloSet()
+    h.nbuf = 1
+    h.bytes[0] = 16
+    assert lib.pcs_halo_exchange(None, 0, 1, ctypes.byref(h), None) == 0
+    assert lib.pcs_halo_exchange(None, 1, 1, ctypes.byref(h), None) == -1
+    assert lib.pcs_halo_exchange(None, 0, 2, ctypes.byref(h), None) == -1  # rank 0 of 2 needs send_hi/recv_hi
+    h.nbuf = 5
+    assert lib.pcs_halo_exchange(None, 0, 1, ctypes.byref(h), None) == -1
