@@ -286,3 +286,51 @@ def test_verbose_lines_fused_match_generic(capsys, verbose):
         assert a['Iter'] == b['Iter']
         for k in list(a)[1:]:
             assert a[k] == b[k] or abs(a[k] - b[k]) <= 1e-9 * abs(b[k]), (k, a, b)
+
+
+def test_pds3d_c4_full_size_fused_vs_generic():
+    """Full C4 size (512^3 fp32, 15-tap Gaussian along every axis, 0.05 L21): the fused 3-D
+    engine (sep2d march + conv0 residual-adjoint + k_pds3d) against the operator-by-operator
+    path for 3 iterations -- same iterates to fp32 rounding, finite, exact count."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.conv import Convolve1D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    from pycsou_amd.opt.proxalgs import PDS
+    n = 512
+    shape, N = (n, n, n), n ** 3
+    g = torch.Generator(device='cuda').manual_seed(3)
+    xs = (torch.rand(shape, generator=g, device='cuda') > 0.5).float()
+    r = np.arange(15) - 7
+    taps = np.exp(-0.5 * (r / 2.0) ** 2)
+    taps /= taps.sum()
+    C = None
+    for ax in range(3):
+        Ci = Convolve1D(N, taps, reshape_dims=shape, axis=ax)
+        Ci.lipschitz_cst = Ci.diff_lipschitz_cst = 1.0
+        C = Ci if C is None else Ci * C
+    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+    y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda')
+    del xs
+    K = Gradient(shape=shape, kind='forward')
+    K.lipschitz_cst = K.diff_lipschitz_cst = np.sqrt(12.0)
+    H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
+    out = []
+    for eng in ['fused', 'generic']:
+        pds = PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, device='cuda'), z0=torch.zeros(3 * N, device='cuda'),
+                  max_iter=2, min_iter=2, accuracy_threshold=0.0, verbose=None, engine=eng)
+        est, _, diag = pds.iterate()
+        assert pds.iter == 3
+        if eng == 'fused':
+            assert isinstance(pds._engine, PDS3DEngine)
+        out.append((est['primal_variable'], est['dual_variable'],
+                    diag['Relative Improvement (primal variable)'].to_numpy(float)))
+        del pds, est
+        torch.cuda.empty_cache()
+    for k in range(2):
+        d = float(torch.linalg.vector_norm(out[0][k] - out[1][k]) / torch.linalg.vector_norm(out[1][k]))
+        assert d < 3e-5, (k, d)
+    assert torch.isfinite(out[0][0]).all() and torch.isfinite(out[0][1]).all()
+    np.testing.assert_allclose(out[0][2][1:], out[1][2][1:], rtol=1e-3)
