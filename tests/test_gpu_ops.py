@@ -364,3 +364,18 @@ def test_apgd_step(A, dtype, gkind, n):
     xn_h = host(xn).astype(np.float64)
     assert abs(d2 - np.sum((x.astype(np.float64) - xn_h) ** 2)) <= 1e-9 * max(1.0, d2)
     assert abs(n2 - np.sum(x.astype(np.float64) ** 2)) <= 1e-9 * n2
+
+
+def test_convolve1d_lipschitz_doctest(A):
+    """Known answers of core/linop.py:262-266 and 299-303 (Convolve1D of a half-zeroed 5-tap
+    Hann window on a 30-sample signal): three largest singular values round to 0.5 and the
+    Lipschitz constant rounds to 0.5."""
+    from scipy import signal
+    from pycsou_amd.linop.conv import Convolve1D
+    sig = np.repeat([0., 1., 0.], 10)
+    filt = signal.windows.hann(5)
+    filt[filt.size // 2:] = 0
+    op = Convolve1D(size=sig.size, filter=filt)
+    np.testing.assert_array_equal(np.round(op.singularvals(k=3, which='LM', tol=1e-3), 2), [0.5, 0.5, 0.5])
+    op.compute_lipschitz_cst(tol=1e-2)
+    assert np.round(op.lipschitz_cst, 1) == 0.5
