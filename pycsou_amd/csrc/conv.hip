@@ -601,11 +601,12 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
 // zeros outside the plane) is loaded from HBM once per strip, staged in LDS, its horizontal
 // pass (taps hb) lands in a 32-row LDS ring, and the vertical pass (taps ha) of 16 output rows
 // reads the ring: no vertical halo is recomputed (k_sep2d re-reads and re-filters 14 halo rows
-// per 32-row tile).  Work: the rows of all (plane, strip) pieces, flattened (row fastest) and
-// cut into one equal contiguous range per resident workgroup; a range that crosses into the
-// next piece restarts the march there (14 rows of prologue).  The XCD-aware block -> range map
-// keeps neighbouring strips (which share 20 halo columns) on one XCD at the same time.
-// Sums are k_sep2d's (t ascending per output): identical results for the H-first order.
+// per 32-row tile).  Work: tasks = (plane, row segment, strip), strip fastest, about 8 per
+// resident workgroup (persistent loop; each task restarts the march: 14 rows of prologue).  The
+// XCD-aware map gives the blocks of one XCD consecutive tasks at any moment, i.e. neighbouring
+// strips of the same rows: the 128-B lines of the 20 halo columns they share are read from HBM
+// once and hit the XCD's L2 for the neighbour (PMC: 1.43x the input bytes when neighbouring
+// strips ran at different rows).  Sums are k_sep2d's (t ascending per output).
 template <typename T>
 struct SepM {
   // fp32: 32 rows per step (one step's loads must cover the HBM latency: ~19 KB per block in
@@ -617,15 +618,16 @@ struct SepM {
   static_assert(G == 32 && (RS / RB) * G == 256, "one vertical item (RB rows) and NH horizontal rows per thread");
 };
 
-struct SepCur {  // a step of the march: piece (plane * nstrips + strip), rows [a, b), step s of ns
-  int64_t piece;
-  int a, b, s, ns;
+struct SepCur {  // a step of the march: task t (plane, segment, strip), rows [a, b), step s of ns
+  int64_t t, plane;
+  int strip, a, b, s, ns;
 };
 
 template <typename T, int SHIFT, bool VEC>
 __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T* __restrict__ out, int n1, int n2,
-                                                     int nstrips, int64_t total, const T* __restrict__ ha_, int ka,
-                                                     int offa, const T* __restrict__ hb_, int kb, int S0) {
+                                                     int nstrips, int nseg, int seg_len, int64_t ntasks,
+                                                     const T* __restrict__ ha_, int ka, int offa,
+                                                     const T* __restrict__ hb_, int kb, int S0) {
   using S = SepM<T>;
   constexpr int KT = S::KT, TX = S::TX, GI = S::GI, WI = S::WI, RS = S::RS, RING = S::RING, RB = S::RB, NL = S::NL,
                 NH = S::NH;
@@ -638,21 +640,30 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
     ha[t] = t < ka ? ha_[t] : T(0);
     hb[t] = t < kb ? hb_[t] : T(0);
   }
-  // XCD-aware bijective block -> range map: the blocks of XCD (b % 8) take consecutive ranges
-  int64_t task;
+  // XCD-aware task map: XCD x (blocks b % 8 == x, nbx of them) owns a contiguous share of the
+  // task list proportional to nbx; its k-th block takes lo + k, lo + k + nbx, ... so that the
+  // blocks running together on one XCD work on consecutive tasks
+  int64_t t0, t_end, t_stride;
   {
-    const int64_t b = blockIdx.x, nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = b % 8, k = b / 8;
-    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+    const int64_t b = blockIdx.x, nb = gridDim.x, xcd = b % 8, k = b / 8, q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (xcd < r ? 1 : 0);
+    const int64_t before = xcd * q + (xcd < r ? xcd : r);  // blocks of the XCDs below x
+    const int64_t lo = ntasks * before / nb, hi = ntasks * (before + nbx) / nb;
+    t0 = lo + k;
+    t_end = hi;
+    t_stride = nbx;
   }
-  const int64_t R0 = task * total / gridDim.x, R1 = (task + 1) * total / gridDim.x;
-  if (R0 >= R1) return;
+  if (t0 >= t_end) return;
   const int tid = threadIdx.x, g = tid & 31, hrow = tid >> 5;
-  auto piece_at = [&](int64_t r) {  // the step cursor at flattened row r (< R1)
+  auto task_at = [&](int64_t t) {  // the first step of task t
     SepCur c;
-    c.piece = r / n1;
-    c.a = (int)(r - c.piece * n1);
-    const int64_t end = (c.piece + 1) * n1 < R1 ? (c.piece + 1) * n1 : R1;
-    c.b = (int)(end - c.piece * n1);
+    c.t = t;
+    const int64_t per_plane = (int64_t)nseg * nstrips;
+    c.plane = t / per_plane;
+    const int rem = (int)(t - c.plane * per_plane), seg = rem / nstrips;
+    c.strip = rem - seg * nstrips;
+    c.a = seg * seg_len;
+    c.b = min(n1, c.a + seg_len);
     c.s = 0;
     c.ns = (c.b - c.a + KT - 1 + RS - 1) / RS;
     return c;
@@ -660,9 +671,8 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
   Q4<T> q[NL];
   // loads of step c: input rows k = s RS + rr (global row a + offa - 14 + k) of the piece
   auto prefetch = [&](const SepCur& c) {
-    const int64_t pl = c.piece / nstrips;
-    const int j0 = (int)(c.piece - pl * nstrips) * TX;
-    const T* src = in + pl * (int64_t)n1 * n2;
+    const int j0 = c.strip * TX;
+    const T* src = in + c.plane * (int64_t)n1 * n2;
     const int kmax = c.b - c.a + KT - 2;  // last input row any output of [a, b) reads
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
@@ -685,7 +695,7 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
       }
     }
   };
-  SepCur cur = piece_at(R0);
+  SepCur cur = task_at(t0);
   prefetch(cur);
   for (;;) {
     // staging <- the landed rows of this step (slot e = row * GI + group: pitch WI)
@@ -700,9 +710,8 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
     if (cur.s + 1 < cur.ns) {
       nxt.s = cur.s + 1;
     } else {
-      const int64_t done = cur.piece * n1 + cur.b;
-      more = done < R1;
-      if (more) nxt = piece_at(done);
+      more = cur.t + t_stride < t_end;
+      if (more) nxt = task_at(cur.t + t_stride);
     }
     if (more) prefetch(nxt);
     // horizontal pass: rows hrow + 8 h of the step, output group g -> ring slot of row k
@@ -747,9 +756,8 @@ __global__ __launch_bounds__(256) void k_sep2d_march(const T* __restrict__ in, T
           }
         }
       }
-      const int64_t pl = cur.piece / nstrips;
-      const int gc = (int)(cur.piece - pl * nstrips) * TX + 4 * g;
-      T* dst = out + pl * (int64_t)n1 * n2;
+      const int gc = cur.strip * TX + 4 * g;
+      T* dst = out + cur.plane * (int64_t)n1 * n2;
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         const int o = cur.a - (KT - 1) + cur.s * RS + r0 + r;
@@ -789,16 +797,21 @@ template <typename T>
 static void launch_sep2d_march(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka,
                                int offa, const void* hb, int kb, int offb, hipStream_t st) {
   using S = SepM<T>;
-  const int64_t nstrips = (n2 + S::TX - 1) / S::TX, total = np * nstrips * n1;
+  const int64_t nstrips = (n2 + S::TX - 1) / S::TX, pieces = np * nstrips;
   const int d = offb - (S::KT - 1);  // first tap-window column relative to the output column
   const int S0 = d >= 0 ? 0 : -((-d + 3) / 4) * 4, shift = d - S0;
-  int64_t grid = sep_march_slots<T>();
-  const int64_t by_rows = (total + 63) / 64;  // ranges of at least 64 rows
-  grid = grid < by_rows ? grid : by_rows;
-  grid = grid < 1 ? 1 : grid;
+  const int64_t slots = sep_march_slots<T>();
+  // row segments: about 8 tasks per resident workgroup, segments of >= 32 rows
+  int64_t nseg = (8 * slots + pieces / 2) / pieces;
+  const int64_t max_seg = n1 / 32 > 1 ? n1 / 32 : 1;
+  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
+  const int64_t seg_len = (n1 + nseg - 1) / nseg;
+  nseg = (n1 + seg_len - 1) / seg_len;
+  const int64_t ntasks = pieces * nseg;
+  const int64_t grid = ntasks < slots ? ntasks : slots;
   auto args = [&](auto kern) {
-    kern<<<(unsigned)grid, 256, 0, st>>>((const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, total, (const T*)ha,
-                                         ka, offa, (const T*)hb, kb, S0);
+    kern<<<(unsigned)grid, 256, 0, st>>>((const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg,
+                                         (int)seg_len, ntasks, (const T*)ha, ka, offa, (const T*)hb, kb, S0);
   };
   const bool vec = n2 % 4 == 0;
   switch (shift) {

@@ -115,7 +115,12 @@ __device__ __forceinline__ void gstore(T* p, const G4<T>& g, int c, int n2) {
   }
 }
 
-constexpr int k3T1 = 8, k3TW = 64, k3NT = 256;
+#ifndef PCS_K3TW
+#define PCS_K3TW 128
+#endif
+// 8 x 128 tiles: a 64-column tile's one-group right halo costs a third 128-B line per row
+// (PMC: 1.53x the algorithmic reads); at 128 columns it is one line in five
+constexpr int k3T1 = 8, k3TW = PCS_K3TW, k3NT = PCS_K3TW == 64 ? 256 : PCS_K3TW == 128 ? 512 : 1024;
 
 template <typename T, int FK, bool VEC>
 __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
@@ -342,7 +347,8 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
   const int64_t bands = (L0 > 0) + (L1 > 0);
   // about 8 resident workgroups per CU on 256 CUs; never segments shorter than 8 planes
-  int64_t nseg = (2048 + per_plane - 1) / per_plane;
+  const int64_t target = 2048 * 256 / k3NT;  // about 8 resident 256-thread workgroups per CU
+  int64_t nseg = (target + per_plane - 1) / per_plane;
   const int64_t max_seg = (L + 7) / 8;
   nseg = nseg > max_seg ? max_seg : nseg;
   nseg = nseg < bands ? bands : nseg;
