@@ -14,7 +14,8 @@ halo rows with the two neighbour ranks and all-reduces the four convergence norm
 `value` is the whole-job throughput in 4096^2-image PDS iterations per second
 (= N x slab iterations/s).
 
-Second workload in the same line (`volume_c5`, BASELINE configs[4]): the 1024^3 fp64 3-D
+Volume workloads in the same line (`volume_c4`, `volume_c5`: BASELINE configs[3], [4]): the
+512^3 fp32 and the 1024^3 fp64 3-D
 TV-deconvolution (three 15-tap Convolve1D, 3-D Gradient, 0.05 L21) plane-slab sharded over
 the same N ranks (strong scaling: the whole volume at every N), PDS3DEngine with the banded
 schedule (halo exchange and sums all-gather overlapped with the interior planes).  It runs
@@ -148,7 +149,7 @@ def build_volume(n, dtype, seed=0):
 
 
 def volume_bench(n, dtype, K, W, world, rank):
-    """C5: the whole n^3 volume plane-slab sharded over `world` ranks; K timed iterations
+    """C4 / C5: the whole n^3 volume plane-slab sharded over `world` ranks; K timed iterations
     (barrier + synchronize on both sides, max over ranks)."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     from pycsou_amd.parallel import DistComm
@@ -184,7 +185,7 @@ def volume_bench(n, dtype, K, W, world, rank):
     elem = torch.empty(0, dtype=dtype).element_size()
     alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
     halo = 0 if world == 1 else (eng.hx + 3 * eng.hz) * eng.plane * elem
-    res = {'workload': f'C5 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
+    res = {'workload': f'{"C5" if elem == 8 else "C4"} 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
                        f'(Convolve1D x3), 3-D Gradient(kind=forward), 0.05*L21Norm, PDS3DEngine, '
                        f'{world} plane slab(s) (strong scaling: whole volume at every N)',
            'it_per_s': round(1e3 / ms, 3), 'ms_per_iter': round(ms, 4), 'steps': K, 'warmup': W,
@@ -261,9 +262,8 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--volume-size', type=int, default=1024, help='C5 volume edge (0: skip the volume leg)')
-    ap.add_argument('--volume-dtype', default='f64', choices=['f32', 'f64'])
-    ap.add_argument('--volume-steps', type=int, default=10)
+    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
+                    help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
                     help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
@@ -363,9 +363,10 @@ def main():
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:
             out['cpu_baseline'] = None
-    if args.volume_size > 0:
-        out = volume_leg(args, out if rank == 0 else None, dtype_v=torch.float64 if args.volume_dtype == 'f64'
-                         else torch.float32, world=world, rank=rank)
+    for leg in filter(None, args.volumes.split(',')):
+        name, edge, vdt, vsteps = leg.split(':')
+        out = volume_leg(args, out if rank == 0 else None, f'volume_{name}', int(edge),
+                         torch.float64 if vdt == 'f64' else torch.float32, int(vsteps), world, rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -373,12 +374,12 @@ def main():
         dist.destroy_process_group()
 
 
-def volume_leg(args, out, dtype_v, world, rank):
-    """Run volume_bench under a watchdog; `out` (rank 0) gains `volume_c5`.  A failure leaves
-    the C3 line as it was; a stall past --volume-timeout prints it and ends the process."""
+def volume_leg(args, out, key, edge, dtype_v, steps, world, rank):
+    """Run volume_bench under a watchdog; `out` (rank 0) gains `key`.  A failure leaves the C3
+    line as it was; a stall past --volume-timeout prints it and ends the process."""
     def fire():
         if out is not None:
-            out['volume_c5'] = {'error': f'no result within {args.volume_timeout:.0f} s'}
+            out[key] = {'error': f'no result within {args.volume_timeout:.0f} s'}
             print(json.dumps(out), flush=True)
         sys.stderr.write('bench: volume leg timed out\n')
         sys.stderr.flush()
@@ -387,14 +388,14 @@ def volume_leg(args, out, dtype_v, world, rank):
     timer.daemon = True
     timer.start()
     try:
-        K = max(2, args.volume_steps + args.volume_steps % 2)
-        vres = volume_bench(args.volume_size, dtype_v, K, 2, world, rank)
+        K = max(2, steps + steps % 2)
+        vres = volume_bench(edge, dtype_v, K, 2, world, rank)
     except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
         vres = {'error': f'{type(e).__name__}: {e}'[:300]}
         print(f'bench: volume leg failed: {vres["error"]}', file=sys.stderr)
     timer.cancel()
     if out is not None:
-        out['volume_c5'] = vres
+        out[key] = vres
     return out
 
 
