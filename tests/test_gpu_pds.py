@@ -228,21 +228,21 @@ def test_pds3d_fused_matches_reference(name, dtype):
     assert isinstance(pds._engine, PDS3DEngine)
 
 
-def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10):
+def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None):
     """A 3-D TV deconvolution case (separable 15-tap Gaussian along every axis), built like
     the golden cases so tests/cases.oracle_pds can run it."""
     rng = np.random.default_rng(seed)
-    shape = (n, n, n)
+    shape = (n, n, n) if shape is None else tuple(shape)
     xs = np.zeros(shape)
     for _ in range(12):
-        lo = rng.integers(0, n, 3)
-        hi = np.minimum(n, lo + rng.integers(n // 8, n // 2, 3))
+        lo = np.array([rng.integers(0, m) for m in shape])
+        hi = np.minimum(shape, lo + np.array([rng.integers(max(1, m // 8), max(2, m // 2)) for m in shape]))
         xs[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = rng.uniform(0, 1)
     r = np.arange(15) - 7
     taps = np.exp(-0.5 * (r / 2.0) ** 2)
     taps /= taps.sum()
     from oracle import pylops1 as P
-    N = n ** 3
+    N = int(np.prod(shape))
     v = xs.ravel()
     for a in range(3):
         v = P.Convolve1D(N, taps, offset=7, dims=shape, dir=a).matvec(v)
@@ -334,3 +334,20 @@ def test_pds3d_c4_full_size_fused_vs_generic():
         assert d < 3e-5, (k, d)
     assert torch.isfinite(out[0][0]).all() and torch.isfinite(out[0][1]).all()
     np.testing.assert_allclose(out[0][2][1:], out[1][2][1:], rtol=1e-3)
+
+
+@pytest.mark.parametrize('shape,dtype', [((20, 36, 260), np.float64), ((17, 9, 132), np.float32),
+                                         ((12, 33, 130), np.float64)])
+def test_pds3d_ragged_tiles_vs_oracle(shape, dtype):
+    """Ragged 3-D shapes for the 8 x 128 update tiles and the 128-column sep2d strips: a last
+    column tile of 4 (260, 132: vector path) or 2 columns (130: scalar path), rows not a
+    multiple of 8, against the CPU oracle (8 iterations)."""
+    c = _vol_problem(0, dtype, seed=5, niter=8, shape=shape)
+    pds = build(c, dtype, engine='fused')
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    est, _, diag = pds.iterate()
+    assert pds.iter == 8
+    x_ref, z_ref, d_ref = oracle_pds(c)
+    tol = 1e-10 if dtype == np.float64 else 5e-5
+    assert rel(est['primal_variable'], x_ref) < tol
+    assert rel(est['dual_variable'], z_ref) < tol
