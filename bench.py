@@ -193,6 +193,8 @@ def volume_bench(n, dtype, K, W, world, rank):
            'iteration_frac_of_hbm_peak_per_gpu': round(alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
            'alg_bytes_per_iter': alg, 'halo_bytes_per_side_per_iter': halo,
            'banded_overlap': bool(getattr(eng, 'banded', False) and eng.overlap),
+           'banded_order': getattr(eng, 'order', None) if world > 1 else None,
+           'order_trial_ms': getattr(eng, 'tune_ms', None),
            'setup_s': round(t1 - t0, 1)}
     del eng
     if comm is not None:
@@ -389,7 +391,7 @@ def volume_leg(args, out, key, edge, dtype_v, steps, world, rank):
     timer.start()
     try:
         K = max(2, steps + steps % 2)
-        vres = volume_bench(edge, dtype_v, K, 2, world, rank)
+        vres = volume_bench(edge, dtype_v, K, 6, world, rank)  # warmup also picks the banded order
     except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
         vres = {'error': f'{type(e).__name__}: {e}'[:300]}
         print(f'bench: volume leg failed: {vres["error"]}', file=sys.stderr)

@@ -601,8 +601,9 @@ __global__ __launch_bounds__(256) void k_sep2d(const T* __restrict__ in, T* __re
 // zeros outside the plane) is loaded from HBM once per strip, staged in LDS, its horizontal
 // pass (taps hb) lands in a 32-row LDS ring, and the vertical pass (taps ha) of 16 output rows
 // reads the ring: no vertical halo is recomputed (k_sep2d re-reads and re-filters 14 halo rows
-// per 32-row tile).  Work: tasks = (plane, row segment, strip), strip fastest, about 8 per
-// resident workgroup (persistent loop; each task restarts the march: 14 rows of prologue).  The
+// per 32-row tile).  Work: tasks = (plane, row segment, strip), strip fastest, the segment count
+// from a cost model (waves of resident workgroups x (rows + 14-row prologue) per task), run by
+// a persistent loop (each task restarts the march).  The
 // XCD-aware map gives the blocks of one XCD consecutive tasks at any moment, i.e. neighbouring
 // strips of the same rows: the 128-B lines of the 20 halo columns they share are read from HBM
 // once and hit the XCD's L2 for the neighbour (PMC: 1.43x the input bytes when neighbouring
@@ -801,10 +802,19 @@ static void launch_sep2d_march(const void* in, void* out, int64_t np, int64_t n1
   const int d = offb - (S::KT - 1);  // first tap-window column relative to the output column
   const int S0 = d >= 0 ? 0 : -((-d + 3) / 4) * 4, shift = d - S0;
   const int64_t slots = sep_march_slots<T>();
-  // row segments: about 8 tasks per resident workgroup, segments of >= 32 rows
-  int64_t nseg = (8 * slots + pieces / 2) / pieces;
+  // row segments: the count that minimises (waves of resident workgroups) x (rows per task +
+  // the 14-row prologue), segments of >= 32 rows (thin sub-volumes -- the boundary bands of
+  // the multi-GPU schedule -- get few long segments, large volumes about 8+ tasks per block)
   const int64_t max_seg = n1 / 32 > 1 ? n1 / 32 : 1;
-  nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
+  int64_t nseg = 1, best = -1;
+  for (int64_t c = 1; c <= max_seg; ++c) {
+    const int64_t len = (n1 + c - 1) / c, waves = (pieces * c + slots - 1) / slots;
+    const int64_t cost = waves * (len + S::KT - 1);
+    if (best < 0 || cost < best) {
+      best = cost;
+      nseg = c;
+    }
+  }
   const int64_t seg_len = (n1 + nseg - 1) / nseg;
   nseg = (n1 + seg_len - 1) / seg_len;
   const int64_t ntasks = pieces * nseg;

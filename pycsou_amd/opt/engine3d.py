@@ -25,6 +25,7 @@ ranks all-gather the four norm sums and exchange the x' / z' halo planes.
 """
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -168,6 +169,15 @@ class PDS3DEngine:
         self.banded = (fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and world > 1
                        and self.rows > 2 * self.band) if fk == L.PCS_F_GRADBUF else False
         self.overlap = bool(overlap)
+        # banded order: 'split' = g of the boundary bands before the exchange starts, the
+        # interior's g after (the exchange overlaps the interior g + update); 'fullg' = g on
+        # all planes before the exchange (one axis-0 launch: no extra 28-plane prologues per
+        # band; the exchange overlaps the interior update only).  Same arithmetic either way.
+        self.order = os.environ.get('PCS_3D_ORDER', 'split')
+        # which order wins depends on the link speed (the halo bytes vs the overlap window):
+        # with a real transport the first advance() of >= 5 iterations times both and keeps
+        # the faster (max over ranks), unless PCS_3D_ORDER fixes it
+        self._tuned = 'PCS_3D_ORDER' in os.environ or not getattr(comm, 'tunable', False)
         if fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and self.rows > 2 * self.band:
             # g in a buffer of its own: the banded order writes g on the boundary planes while the
             # interior's axis-0 pass still reads the in-plane forward result around them
@@ -295,8 +305,11 @@ class PDS3DEngine:
         nsub = R + 2 * hx
         self._sep_range(self.X[p], self.T[0], 0, hx, False, st)
         self._sep_range(self.X[p], self.T[0], hx + R, nsub, False, st)
-        self._g_range(hx, hx + B + 1, st)
-        self._g_range(hx + R - B, min(hx + R + 1, nsub), st)
+        if self.order == 'fullg':  # g on every plane the update reads, one axis-0 launch
+            self._g_range(hx, min(hx + R + 1, nsub), st)
+        else:
+            self._g_range(hx, hx + B + 1, st)
+            self._g_range(hx + R - B, min(hx + R + 1, nsub), st)
         a = self.args[p]
         a.hist = None
         a.partials = self.partials.data_ptr()
@@ -304,7 +317,8 @@ class PDS3DEngine:
 
     def _band_interior(self, p, st):
         hx, R, B = self.hx, self.rows, self.band
-        self._g_range(hx + B + 1, hx + R - B, st)
+        if self.order != 'fullg':
+            self._g_range(hx + B + 1, hx + R - B, st)
         a = self.args[p]
         a.hist = None
         a.partials = self.partials.data_ptr() + 32 * self.nb_bands[0]
@@ -439,10 +453,41 @@ class PDS3DEngine:
             for _ in range(k // self.chunk):
                 self.graph.replay()
             return
+        if not self._tuned and self.banded and self.overlap and k >= 5:
+            k -= self._autotune()
         for _ in range(k):
             self.iteration(self._p)
             self._p ^= 1
         self._drain()
+
+    def _autotune(self):
+        """Time 2 iterations in each banded order (after one untimed) and keep the faster;
+        every rank takes the same decision (max over ranks).  Returns the iterations used."""
+        self.iteration(self._p)
+        self._p ^= 1
+        times = []
+        for order in ('split', 'fullg'):
+            self.order = order
+            self._drain()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(2):
+                self.iteration(self._p)
+                self._p ^= 1
+            self._drain()
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        dev = self.sums.device
+        mine = torch.tensor(times + [0.0, 0.0], dtype=torch.float64, device=dev)
+        allt = torch.zeros(4 * self.world, dtype=torch.float64, device=dev)
+        self.comm.allgather(mine, allt)
+        worst = allt.view(self.world, 4).max(dim=0).values
+        self.order = 'split' if float(worst[0]) <= float(worst[1]) else 'fullg'
+        self.tune_ms = [float(worst[0]) / 2, float(worst[1]) / 2]
+        self._tuned = True
+        return 5
 
     def iterations(self):
         return int(self.ctrl.view(torch.int32)[0].item())

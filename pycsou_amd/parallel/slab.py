@@ -50,6 +50,8 @@ def row_split(n0, world, rank):
 class DistComm:
     """Sum gathering and neighbour halo exchange over a torch.distributed group."""
 
+    tunable = True  # a real transport: schedule choices may be timed through it
+
     def __init__(self, group=None):
         self.group = group
         self.rank = dist.get_rank(group)

@@ -141,9 +141,10 @@ def rank_share(args):
     print(f'built in {time.time() - t0:.1f} s', flush=True)
     K = args.steps + args.steps % 2
     out = {'workload': f'one rank ({rank} of {W}) of 3-D TV-deconv {args.size}^3 {args.dtype}'}
-    for name, ov in (('serial', False), ('banded', True)):
+    for name, ov, order in (('serial', False, 'split'), ('banded', True, 'split'), ('banded_fullg', True, 'fullg')):
         eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, comm=NullComm(rank, W),
                           rank=rank, world=W, overlap=ov)
+        eng.order = order
         eng.init_loop(K + 8, K + 8, -1.0)
         eng.advance(4)
         torch.cuda.synchronize()
