@@ -252,7 +252,7 @@ def slab_bench(n, dtype, K, W, world):
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
     loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else 'python'
     return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks,
-            'loop': loop}
+            'loop': loop, 'schedule_trial_ms': getattr(eng, 'tune_ms', None)}
 
 
 def main():
@@ -348,7 +348,8 @@ def main():
                                       and args.engine != 'slab' else
                                       f'slab engine ({res.get("loop", "python")} loop): per-iteration RCCL '
                                       f'all-gather of 4 sums + neighbour halo exchange'),
-                       'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single'},
+                       'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single',
+                       'schedule_trial_ms_serial_overlap': res.get('schedule_trial_ms')},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,
                          'kernel': 'pcs_pds2d_step (k_pds2d_march<float,7,L21,256>)',

@@ -342,3 +342,33 @@ def test_slab3d_two_process_overlap(tmp_path):
     h = np.load(tmp_path / 'hist.npy')
     fin = np.isfinite(h1)
     assert np.allclose(h[fin], h1[fin], rtol=1e-12)
+
+
+class _CopyComm:
+    """One-rank stand-in transport for exercising the schedule trial (allgather = copy)."""
+    tunable = True
+
+    def allgather(self, src, dst):
+        dst[:src.numel()].copy_(src)
+
+
+@pytest.mark.parametrize('kind', ['deconv', 'denoise'])
+def test_native_schedule_trial_bitwise(kind):
+    """SlabPDS2D._autotune (serial vs overlapped native schedule, timed, plan switched in the
+    middle of the loop) keeps the iteration count and gives bitwise the single-GPU iterates."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.parallel import SlabPDS2D
+    pds = _problem(kind)
+    spec = pds._fused_spec()
+    eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    n, x1, z1, _ = eng.run(29, 29, 0.0)
+    s = SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, 0, 1, native=True,
+                  overlap=True, chunk=7)
+    s.comm = _CopyComm()
+    total = s.init_loop(29, 29, 0.0)
+    used = s._autotune()
+    assert used == 8 and s._tuned and len(s.tune_ms) == 2
+    s.advance(total - used)
+    n2, x2, z2, _ = s.result()
+    assert n2 == n == 30
+    assert torch.equal(x2, x1) and torch.equal(z2, z1)
