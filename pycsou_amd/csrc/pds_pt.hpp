@@ -74,7 +74,16 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
   }
   G4<T> xr, gr, zr0[KZ0], zr1[KZ1];
   T xre = T(0), gre = T(0);
-  auto loads = [&](int a) {  // x, y|g on the P45 row a + 1 + ui; z rows [a, a + TS]
+  // loads of step a, in two parts so that each is issued as soon as its registers are free:
+  // z rows [a, a + TS] right after the previous step's z landed in LDS, x and y|g on the P45
+  // row a + 1 + ui right after the previous step's P45 used them
+  auto loads_z = [&](int a) {
+#pragma unroll
+    for (int k = 0; k < KZ0; ++k) zr0[k] = bload4(vz0.r, vz0.row_off(a + rr_z0[k]) + co_z0[k]);
+#pragma unroll
+    for (int k = 0; k < KZ1; ++k) zr1[k] = bload4(vz1.r, vz1.row_off(a + rr_z1[k]) + co_z1[k]);
+  };
+  auto loads_x = [&](int a) {
     const uint32_t ro = vx.row_off(a + 1 + ui);
     xr = bload4(vx.r, ro + co_u);
     xre = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vx.r, (int)(ro + co_e), 0, 0));
@@ -83,10 +92,6 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
       gr = bload4(vg.r, rg + co_u);
       gre = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vg.r, (int)(rg + co_e), 0, 0));
     }
-#pragma unroll
-    for (int k = 0; k < KZ0; ++k) zr0[k] = bload4(vz0.r, vz0.row_off(a + rr_z0[k]) + co_z0[k]);
-#pragma unroll
-    for (int k = 0; k < KZ1; ++k) zr1[k] = bload4(vz1.r, vz1.row_off(a + rr_z1[k]) + co_z1[k]);
   };
   auto land_z = [&]() {
 #pragma unroll
@@ -197,21 +202,24 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
   };
 
   // prologue: u on row s0 (step a = s0 - TS, row TS - 1 of its P45), x' on row s0
-  loads(s0 - TS);
+  const int nsteps = (s1 - s0 + TS - 1) / TS;
+  loads_z(s0 - TS);
+  loads_x(s0 - TS);
   land_z();
+  if (nsteps > 0) loads_z(s0);
   lds_barrier();
   p45(s0 - TS, launder(flags), 1);
-  const int nsteps = (s1 - s0 + TS - 1) / TS;
+  if (nsteps > 0) loads_x(s0);
   int ub = 0;
-  if (nsteps > 0) loads(s0);
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
     const int fl = launder(flags);
     lds_barrier();  // previous P6 done with Z, U rows
     land_z();
+    if (k + 1 < nsteps) loads_z(a + TS);  // next step's z flies during this step's P45 and P6
     lds_barrier();
     p45(a, fl, ub);
-    if (k + 1 < nsteps) loads(a + TS);  // next step's loads fly during this step's P6
+    if (k + 1 < nsteps) loads_x(a + TS);  // next step's x, y|g during this step's P6
     lds_barrier();
     p6(a, fl, ub);
     ub = ub == 0 ? 16 : ub - 1;
