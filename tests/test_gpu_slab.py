@@ -372,3 +372,30 @@ def test_native_schedule_trial_bitwise(kind):
     n2, x2, z2, _ = s.result()
     assert n2 == n == 30
     assert torch.equal(x2, x1) and torch.equal(z2, z1)
+
+
+def test_rccl_binding_world1():
+    """The run-time RCCL binding behind the native multi-GPU loops (dlopen of librccl, unique
+    id, communicator init/destroy) on a one-rank communicator, plus pcs_halo_exchange and a
+    native slab plan on it: the path the driver's multi-GPU bench takes first."""
+    import ctypes
+    from pycsou_amd import _lib as L
+    from pycsou_amd.parallel import SlabPDS2D
+    lib = L.gpu()
+    assert lib.pcs_comm_available() == 1
+    nb = int(lib.pcs_comm_id_bytes())
+    assert nb == 128  # sizeof(ncclUniqueId)
+    uid = (ctypes.c_ubyte * nb)()
+    assert lib.pcs_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)) == 0
+    assert any(uid)
+    h = ctypes.c_void_p()
+    assert lib.pcs_comm_init(ctypes.cast(uid, ctypes.c_void_p), 1, 0, ctypes.byref(h)) == 0 and h.value
+    hs = L.HaloSet()
+    assert lib.pcs_halo_exchange(h, 0, 1, ctypes.byref(hs), L.stream()) == 0
+    pds = _problem('denoise')
+    spec = pds._fused_spec()
+    s = SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, 0, 1, native=True)
+    n, x, z, _ = s.run(9, 9, 0.0)
+    assert n == 10 and torch.isfinite(x).all()
+    torch.cuda.synchronize()
+    assert lib.pcs_comm_destroy(h) == 0
