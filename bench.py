@@ -102,8 +102,9 @@ def cpu_baseline(n, iters):
            max_iter=iters - 1, min_iter=iters - 1, accuracy_threshold=0.0, pandas_diagnostics=True)
     dt = time.perf_counter() - t0
     return {'value': iters / dt, 'unit': 'it/s', 'cores': 1, 'kind': 'port', 'host_cpus': os.cpu_count(),
-            'validation': 'this restatement ran 0.86-0.94x the real reference time per iteration, identical '
-                          'iterates, on 512^2-2048^2 (anisotropic-L1 variant; tests/golden/cpu_baseline_check.json); '
+            'validation': 'this restatement ran 0.80-0.96x the real reference time per iteration (0.94x at '
+                          '4096^2), identical iterates, on 512^2-4096^2 (anisotropic-L1 variant; '
+                          'tests/golden/cpu_baseline_check.json); '
                           'the reference isotropic L21 is an O(G N) Python loop: 1.29 s/iter at 128^2, '
                           'extrapolated ~1.4e6 s/iter at 4096^2, so the L21 prox here is vectorised',
             'sample': f'{iters} PDS iterations of the same 4096x4096 TV-deconvolution (fp64, reference op '

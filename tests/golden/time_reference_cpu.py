@@ -80,7 +80,7 @@ def main():
     R = import_reference()
     out = {'host': {'nproc': os.cpu_count(), 'OMP_NUM_THREADS': os.environ.get('OMP_NUM_THREADS')},
            'anisotropic_l1': [], 'isotropic_l21_reference': []}
-    for n, iters in ((512, 3), (1024, 3), (2048, 3)):
+    for n, iters in ((512, 3), (1024, 3), (2048, 3), (4096, 2)):
         tr, xr = time_reference(R, n, 'l1', iters)
         ts, xs = time_restatement(n, iters)
         rel = float(np.linalg.norm(xr - xs) / np.linalg.norm(xr))
