@@ -105,8 +105,8 @@ def cpu_baseline(n, iters):
             'validation': 'this restatement ran 0.80-0.96x the real reference time per iteration (0.94x at '
                           '4096^2), identical iterates, on 512^2-4096^2 (anisotropic-L1 variant; '
                           'tests/golden/cpu_baseline_check.json); '
-                          'the reference isotropic L21 is an O(G N) Python loop: 1.29 s/iter at 128^2, '
-                          'extrapolated ~1.4e6 s/iter at 4096^2, so the L21 prox here is vectorised',
+                          'the reference isotropic L21 is an O(G N) Python loop: 0.88 s/iter at 128^2, '
+                          'extrapolated ~9e5 s/iter at 4096^2, so the L21 prox here is vectorised',
             'sample': f'{iters} PDS iterations of the same 4096x4096 TV-deconvolution (fp64, reference op '
                       f'sequence incl. SciPy FFT convolution, vectorised pixel-L21, pandas diagnostics, deepcopy) '
                       f'in {dt:.1f} s on 1 host core'}
