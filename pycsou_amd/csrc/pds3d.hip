@@ -9,7 +9,7 @@
 // last sample 0; adjoint accumulated in axis order).
 //
 // Layout: C-order volume (n0 planes of n1 x n2); z = [D0 x; D1 x; D2 x], each component with
-// the same (halo'd) plane layout.  A workgroup owns an 8 x 64 in-plane tile and marches down a
+// the same (halo'd) plane layout.  A workgroup owns an 8 x 128 in-plane tile and marches down a
 // segment of planes: at plane p it lands z(p) in LDS, computes x_t / u on the tile plus one
 // row / one 4-group of halo (u of plane p in a 2-plane LDS ring), writes x'(p), and then
 // z'(p-1), whose axis-0 difference needs u(p).  Loads for plane p+1 are issued before plane
