@@ -198,7 +198,11 @@ typedef struct {
   void* ctrl;             /* device control block (pcs_ctrl_*) ; NULL = always run */
   double* hist;           /* non-NULL: reduce the partials and run pcs_pds_finalize inside the
                              step launch (single GPU); NULL: only write `partials` */
-  void* ws;               /* with hist: pcs_pds2d_ws_bytes() bytes, zeroed once before first use */
+  void* ws;               /* with hist or sums_out: pcs_pds2d_ws_bytes() bytes, zeroed once before first use */
+  double* sums_out;       /* hist NULL, sums_out non-NULL (slab mode): the last workgroups reduce the
+                             partials, then add pre_partials, into sums_out[4] (no loop control) */
+  const double* pre_partials; /* [n_pre][4] partials of an earlier launch of the same iteration */
+  int64_t n_pre;
 } pcs_pds2d_args;
 
 int pcs_pds2d_halo_x(int half);

@@ -36,7 +36,8 @@ class PdsArgs(ctypes.Structure):
                 ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
                 ('step0', _c_dbl), ('step1', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
-                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp),
+                ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64)]
 
 
 class Pds3Args(ctypes.Structure):

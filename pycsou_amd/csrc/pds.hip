@@ -126,6 +126,10 @@ static Params<T> make_params(const pcs_pds2d_args* a) {
   return P;
 }
 
+static RedOut red_out(const pcs_pds2d_args* a) {
+  return a->hist ? RedOut{nullptr, nullptr, 0} : RedOut{a->sums_out, a->pre_partials, (int)a->n_pre};
+}
+
 template <typename T, int FK, int H>
 static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   constexpr int TH = Tile<T>::TH, NT = Tile<T>::NT;
@@ -137,8 +141,8 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   const Params<T> P = make_params<T>(a);
   k_pds2d<T, FK, H, TH, NT><<<(unsigned)ntiles, NT, 0, st>>>(
       (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->y, (const T*)a->gbuf, (const T*)a->taps0,
-      (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, tiles_x,
-      (int)ntiles, tiles_x, 0);
+      (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
+      tiles_x, (int)ntiles, tiles_x, 0);
   return launch_status();
 }
 
@@ -233,7 +237,7 @@ static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
-      a->ws, p.tiles_x, p.bd, p.ntasks);
+      a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
   return launch_status();
 }
 
@@ -293,7 +297,7 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
   k_pds2d_pt<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z,
                                                          (float*)a->zn, g, s, P, a->gkind, a->partials,
-                                                         (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles_x, p.bd,
+                                                         (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd,
                                                          p.ntasks);
   return launch_status();
 }
@@ -373,6 +377,10 @@ int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a) {
 static int check_args(const pcs_pds2d_args* a) {
   if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
   if (a->hist && (!a->ws || !a->ctrl || !aligned16(a->ws) || !aligned16(a->partials))) return PCS_EINVAL;
+  if (!a->hist && a->sums_out &&
+      (!a->ws || !aligned16(a->ws) || !aligned16(a->partials) || a->n_pre < 0 || a->n_pre > 0x7fffffff ||
+       (a->n_pre > 0 && !a->pre_partials)))
+    return PCS_EINVAL;
   if (a->n0 < 1 || a->n1 < 1 || a->rows < 1 || a->row0 < 0 || a->row0 + a->rows > a->n0) return PCS_EINVAL;
   if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return PCS_EINVAL;
   if (a->gkind < PCS_G_NULL || a->gkind > PCS_G_SEGMENT) return PCS_EINVAL;

@@ -64,10 +64,33 @@ __device__ __forceinline__ unsigned drained_add(unsigned* cnt) {
   return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Reduce-only output of the in-kernel reduction (slab mode): the four sums go to `sums`, after
+// adding `npre` partials of an earlier launch of the same iteration; no loop control.
+struct RedOut {
+  double* sums;
+  const double* pre;
+  int npre;
+};
+
+// Entry test of a step kernel against the sticky stop flag (solver.py:65-66): true = skip the
+// iterate update.  Plain launches return at once.  A reduce-only launch (slab overlap mode) can
+// run while the side stream's loop control writes the flag, so thread 0's reading is broadcast
+// and every workgroup still arrives at the reduction counters (with zero partials), which
+// then stay consistent for the next run of the plan.
+__device__ __forceinline__ bool stop_requested(const Ctrl* ctrl, const RedOut& ro, int* flag) {
+  if (ctrl == nullptr) return false;
+  if (ro.sums == nullptr) return ctrl->stopped != 0;
+  if (threadIdx.x == 0) flag[0] = __hip_atomic_load(&ctrl->stopped, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return flag[0] != 0;
+}
+
 // Called by every thread of every workgroup after thread 0's `part` holds the block sums.
-// `flag` is a 2-int LDS scratch.
+// `flag` is a 2-int LDS scratch.  With ro.sums the last group writes the sums instead of
+// running finalize_from.
 __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], double* __restrict__ partials,
-                                                    int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag) {
+                                                    int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag,
+                                                    RedOut ro = RedOut{nullptr, nullptr, 0}) {
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t ngr = red_groups(nblocks);
@@ -108,6 +131,20 @@ __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], dou
   }
   __shared__ double red2[4 * 16];
   block_sum<4>(v, red2);
+  if (ro.sums != nullptr) {  // reduce-only: + the earlier launch's partials (fixed order)
+    double w[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = tid; j < ro.npre; j += blockDim.x) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] += ro.pre[(int64_t)j * 4 + k];
+    }
+    block_sum<4>(w, red2);
+    if (tid == 0) {
+      __hip_atomic_store(&cnt[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ro.sums[k] = v[k] + w[k];
+    }
+    return;
+  }
   if (tid == 0) {
     __hip_atomic_store(&cnt[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     finalize_from(v, ctrl, hist);

@@ -593,18 +593,19 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
 }
 
 // One block per task (64-column strip x row segment); with `hist` the last workgroups also
-// reduce the partials and run the loop control.
+// reduce the partials and run the loop control, with `ro.sums` they only reduce.
 template <typename T, int H, int HK, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_pds2d_march(
     const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
     const T* __restrict__ y, const T* __restrict__ taps0, const T* __restrict__ taps1, int half, Slab32 s,
-    Params<T> P, int gk, double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws, int tiles_x,
-    Bands bd, int ntasks) {
+    Params<T> P, int gk, double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws, RedOut ro,
+    int tiles_x, Bands bd, int ntasks) {
   using M = March<H>;
   __shared__ __attribute__((aligned(16))) T sm[M::SZ];
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
-  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
   int task;
@@ -618,10 +619,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
   const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  march_task<T, H, HK, NT>(x, xn, z, zn, y, taps0, taps1, half, s, P, gk, s0, s1, c0, sm, part);
+  if (!stopped) march_task<T, H, HK, NT>(x, xn, z, zn, y, taps0, taps1, half, s, P, gk, s0, s1, c0, sm, part);
   block_sum<4>(part, red);
-  if (hist != nullptr) {  // single launch per iteration: the last workgroups reduce + finalize
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
+  if (hist != nullptr || ro.sums != nullptr) {  // the last workgroups reduce (+ finalize)
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
   } else if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];

@@ -233,11 +233,12 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
                                                    const float* __restrict__ z, float* __restrict__ zn,
                                                    const float* __restrict__ gsrc, Slab32 s, Params<float> P, int gk,
                                                    double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
-                                                   int tiles_x, Bands bd, int ntasks) {
+                                                   RedOut ro, int tiles_x, Bands bd, int ntasks) {
   __shared__ __attribute__((aligned(16))) float sm[PtGeom::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
-  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
   int task;
   {  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
     const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
@@ -247,10 +248,10 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
   int s0, s1;
   band_rows(bd, seg, s0, s1);
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  pt_task<FK, HK>(x, xn, z, zn, gsrc, s, P, gk, s0, s1, strip * PtGeom::TW, sm, part);
+  if (!stopped) pt_task<FK, HK>(x, xn, z, zn, gsrc, s, P, gk, s0, s1, strip * PtGeom::TW, sm, part);
   block_sum<4>(part, red);
-  if (hist != nullptr) {
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
+  if (hist != nullptr || ro.sums != nullptr) {
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
   } else if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];

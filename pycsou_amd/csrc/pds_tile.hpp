@@ -472,7 +472,7 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
                                                const T* __restrict__ gbuf, const T* __restrict__ taps0,
                                                const T* __restrict__ taps1, int half, Slab s, Params<T> P, int hk,
                                                int gk, double* __restrict__ partials, Ctrl* ctrl,
-                                               double* hist, void* ws, int tiles_x, int ntiles, int bl,
+                                               double* hist, void* ws, RedOut ro, int tiles_x, int ntiles, int bl,
                                                int tx_shift) {
   constexpr bool CONV = (FK == PCS_F_SEPCONV);
   constexpr int TW = 64;
@@ -487,7 +487,8 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
 
-  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent tiles.
   int tile;
@@ -516,14 +517,15 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
                         (t0 - rh >= -hmin) && (t0 + TH + rh <= s.rows - 1 + hmin) && (t0 + TH <= s.rows - 1) &&
                         (c0 - ch >= 0) && (c0 + WG + ch <= s.n1 - 1);
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  if (interior)
+  if (stopped) {
+  } else if (interior)
     pds2d_tile<T, FK, H, TH, NT, true>(x, xn, z, zn, y, gbuf, w0, w1, s, P, hk, gk, t0, c0, bufX, bufA, part);
   else
     pds2d_tile<T, FK, H, TH, NT, false>(x, xn, z, zn, y, gbuf, w0, w1, s, P, hk, gk, t0, c0, bufX, bufA, part);
   block_sum<4>(part, red);
-  if (hist != nullptr) {
-    // single launch per iteration: last workgroups reduce + finalize in-kernel
-    reduce_and_finalize(part, partials, ntiles, ws, ctrl, hist, flag);
+  if (hist != nullptr || ro.sums != nullptr) {
+    // single launch per iteration: last workgroups reduce (+ finalize) in-kernel
+    reduce_and_finalize(part, partials, ntiles, ws, ctrl, hist, flag, ro);
   } else if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];

@@ -27,6 +27,7 @@
 #include <new>
 
 #include "common.hpp"
+#include "pds_ctrl.hpp"
 
 namespace pcs {
 
@@ -74,6 +75,7 @@ struct Slab2DPlan {
   double* partials;   // [nB + nI] (overlap) or [nfull] partial rows of 4
   double* sums;       // [2][4]
   double* gathered;   // [2][4 world]
+  void* ws;           // in-kernel reduction workspace (red_ws_bytes of the reducing launch)
   int64_t nfull, nB, nI;
   bool overlap;
 };
@@ -133,9 +135,11 @@ static int run_serial(Slab2DPlan& P, int64_t n, int p0, hipStream_t st) {
     pcs_pds2d_args a = P.d.step[p];
     a.partials = P.partials;
     a.hist = nullptr;
-    a.ws = nullptr;
+    a.ws = P.ws;  // the step's last workgroups reduce this rank's partials into sums[p]
+    a.sums_out = P.sums + 4 * p;
+    a.pre_partials = nullptr;
+    a.n_pre = 0;
     int rc = pcs_pds2d_step(&a, st);
-    if (rc == PCS_OK) rc = pcs_reduce_partials(P.partials, P.nfull, P.sums + 4 * p, st);
     if (rc == PCS_OK) rc = sums_and_finalize(P, p, st);
     if (rc == PCS_OK) rc = halo_exchange(P, P.d.halo[p], st);
     if (rc != PCS_OK) return rc;
@@ -153,6 +157,7 @@ static int run_overlap(Slab2DPlan& P, int64_t n, int p0, hipStream_t st) {
     pcs_pds2d_args a = P.d.step[p];
     a.hist = nullptr;
     a.ws = nullptr;
+    a.sums_out = nullptr;
     // boundary bands: they read the halo rows of iteration i-1
     if (i > 0 && hipStreamWaitEvent(st, P.ev_halo, 0) != hipSuccess) return PCS_ELAUNCH;
     a.partials = P.partials;
@@ -164,10 +169,13 @@ static int run_overlap(Slab2DPlan& P, int64_t n, int p0, hipStream_t st) {
     rc = halo_exchange(P, P.d.halo[p], P.side);
     if (rc != PCS_OK) return rc;
     if (hipEventRecord(P.ev_halo, P.side) != hipSuccess) return PCS_ELAUNCH;
-    // interior band + this rank's sums
+    // interior band; its last workgroups reduce its partials + the boundary bands' into sums[p]
     a.partials = P.partials + 4 * P.nB;
+    a.ws = P.ws;
+    a.sums_out = P.sums + 4 * p;
+    a.pre_partials = P.partials;
+    a.n_pre = P.nB;
     rc = pcs_pds2d_step_bands(&a, b, R - b, R - b, R - b, st);
-    if (rc == PCS_OK) rc = pcs_reduce_partials(P.partials, P.nB + P.nI, P.sums + 4 * p, st);
     if (rc != PCS_OK) return rc;
     if (hipEventRecord(P.ev_sum, st) != hipSuccess) return PCS_ELAUNCH;
     // side: norms across ranks + stopping rule (the next boundary launch does not wait for it)
@@ -190,6 +198,7 @@ static void destroy_plan(Slab2DPlan* P) {
   if (P->partials) (void)hipFree(P->partials);
   if (P->sums) (void)hipFree(P->sums);
   if (P->gathered) (void)hipFree(P->gathered);
+  if (P->ws) (void)hipFree(P->ws);
   delete P;
 }
 
@@ -238,6 +247,7 @@ int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan) {
   pcs_pds2d_args a = d->step[0];
   a.hist = nullptr;
   a.ws = nullptr;
+  a.sums_out = nullptr;
   a.partials = (double*)d->ctrl;  // non-null placeholder for the argument checks
   P->nfull = pcs_pds2d_nblocks(&a);
   const int64_t R = a.rows, b = d->band;
@@ -248,9 +258,11 @@ int pcs_slab2d_create(const pcs_slab2d_desc* d, void* comm, void** plan) {
     P->overlap = P->nB > 0 && P->nI > 0;
   }
   const int64_t np = P->overlap ? P->nB + P->nI : P->nfull;
+  const int64_t wsb = red_ws_bytes(P->overlap ? P->nI : P->nfull);
   bool ok = P->nfull > 0 && hipMalloc(&P->partials, (size_t)np * 4 * sizeof(double)) == hipSuccess &&
             hipMalloc(&P->sums, 8 * sizeof(double)) == hipSuccess &&
-            hipMalloc(&P->gathered, (size_t)8 * d->world * sizeof(double)) == hipSuccess;
+            hipMalloc(&P->gathered, (size_t)8 * d->world * sizeof(double)) == hipSuccess &&
+            hipMalloc(&P->ws, (size_t)wsb) == hipSuccess && hipMemset(P->ws, 0, (size_t)wsb) == hipSuccess;
   if (ok && P->overlap) {
     ok = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) == hipSuccess;
     hipEvent_t* evs[] = {&P->ev_fork, &P->ev_b, &P->ev_halo, &P->ev_sum, &P->ev_join};

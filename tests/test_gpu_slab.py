@@ -281,6 +281,14 @@ def test_native_loop_early_stop(overlap):
     n2, x2, z2, h2 = s.run(400, 5, 2e-3)
     assert n2 == n
     assert torch.equal(x2, x1) and torch.equal(z2, z1)
+    # the plan runs again after a stop: the step kernels' in-kernel reduction counters (every
+    # workgroup still arrives once the flag is set) are consistent for the next run
+    n, x1, z1, h1 = eng.run(9, 9, 0.0)
+    n2, x2, z2, h2 = s.run(9, 9, 0.0)
+    assert n2 == n == 10
+    assert torch.equal(x2, x1) and torch.equal(z2, z1)
+    assert np.isfinite(h2[:2 * n]).all()
+    assert np.allclose(h2[1:2 * n], h1[1:2 * n], rtol=1e-5)
 
 
 def vol3d_case(n0=80, seed=3, niter=8):

@@ -119,3 +119,31 @@ def test_halo_exchange_argument_checks():
     assert lib.pcs_halo_exchange(None, 0, 2, ctypes.byref(h), None) == -1  # rank 0 of 2 needs send_hi/recv_hi
     h.nbuf = 5
     assert lib.pcs_halo_exchange(None, 0, 1, ctypes.byref(h), None) == -1
+
+
+def test_pds2d_reduce_only_argument_checks():
+    """Slab reduce-only mode of pcs_pds2d_step (sums_out): the host checks reject a missing or
+    misaligned workspace, a negative pre-partials count and pre partials without a pointer,
+    before anything is launched (fake device addresses are never dereferenced)."""
+    import ctypes
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    a = _lib.PdsArgs()
+    a.dtype, a.fkind, a.hkind, a.gkind = _lib.PCS_F32, _lib.PCS_F_DENOISE, _lib.PCS_H_L21, _lib.PCS_G_NULL
+    a.n0 = a.n1 = a.rows = 64
+    a.sigma = a.step0 = a.step1 = 1.0
+    for f in ('x', 'xn', 'z', 'zn', 'y', 'partials'):
+        setattr(a, f, 0x10000)
+    a.sums_out = 0x20000
+    a.hist = None
+    a.ws = None
+    assert lib.pcs_pds2d_step(ctypes.byref(a), None) == -1  # no workspace
+    a.ws = 0x30008
+    assert lib.pcs_pds2d_step(ctypes.byref(a), None) == -1  # misaligned workspace
+    a.ws = 0x30000
+    a.n_pre = -1
+    assert lib.pcs_pds2d_step(ctypes.byref(a), None) == -1
+    a.n_pre = 4
+    a.pre_partials = None
+    assert lib.pcs_pds2d_step(ctypes.byref(a), None) == -1
+    assert lib.pcs_pds2d_step_bands(ctypes.byref(a), 0, 8, 56, 64, None) == -1
