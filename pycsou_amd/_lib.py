@@ -103,6 +103,8 @@ _SIGS = {
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
+    'pcs_pds2d_run_persistent': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp, _vp]),
+    'pcs_grid_bar_bytes': (_c_i64, []),
     'pcs_pds2d_nblocks_bands': (_c_i64, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64]),
     'pcs_pds2d_step_bands': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64, _vp]),
     'pcs_comm_available': (_c_int, []),

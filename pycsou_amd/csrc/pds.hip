@@ -302,6 +302,35 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   return launch_status();
 }
 
+// persistent form: all n iterations in one launch; the grid must be co-resident
+template <int FK, int HK>
+static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hipStream_t st) {
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_pt_loop<FK, HK>, 256, 0) != hipSuccess)
+    return PCS_ELAUNCH;
+  const int tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
+  if (tiles_x < 2 || nb < 1) return PCS_EUNSUPPORTED;
+  MarchPlan p;  // one wave of this kernel's resident workgroups
+  plan_bands(full_bands(a), PtGeom::TS, tiles_x, cus * nb, 4, &p);
+  if (p.ntasks < 1 || (int64_t)p.ntasks > (int64_t)cus * nb) return PCS_EUNSUPPORTED;
+  const Slab s64 = make_slab(a);
+  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
+  const Params<float> P = make_params<float>(a);
+  const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
+  k_pds2d_pt_loop<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
+      (float*)a->x, (float*)a->xn, (float*)a->z, (float*)a->zn, g, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl,
+      a->hist, a->ws, bar, (int)n, p.tiles_x, p.bd, p.ntasks);
+  return launch_status();
+}
+
+template <int FK>
+static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hipStream_t st) {
+  return a->hkind == PCS_H_L21 ? launch_pt_loop<FK, PCS_H_L21>(a, n, bar, st)
+                               : launch_pt_loop<FK, PCS_H_L1>(a, n, bar, st);
+}
+
 template <int FK>
 static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, rb, st) : launch_pt<FK, PCS_H_L1>(a, rb, st);
@@ -442,6 +471,24 @@ int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t st) {
   }
   return PCS_OK;
 }
+
+// The same n iterations as pcs_pds2d_run in ONE launch of the pointwise-F row-marching kernel
+// (fp32 NULL / DENOISE / GRADBUF families), a grid barrier per iteration in place of the
+// kernel boundary.  `bar`: pcs_grid_bar_bytes() device bytes, zeroed once before first use.
+// PCS_EUNSUPPORTED when the problem is not of that family or its grid is not co-resident.
+int pcs_pds2d_run_persistent(const pcs_pds2d_args* a, int64_t n, void* bar, hipStream_t st) {
+  if (!a || n < 0 || n > 0x7fffffff || !a->hist || !bar || !aligned16(bar)) return PCS_EINVAL;
+  const int rc = check_args(a);
+  if (rc != PCS_OK) return rc;
+  if (a->rows != a->n0 || use_march(a) || !use_pt(a)) return PCS_EUNSUPPORTED;
+  if (n == 0) return PCS_OK;
+  unsigned* b = (unsigned*)bar;
+  if (a->fkind == PCS_F_DENOISE) return launch_pt_loop<PCS_F_DENOISE>(a, n, b, st);
+  if (a->fkind == PCS_F_GRADBUF) return launch_pt_loop<PCS_F_GRADBUF>(a, n, b, st);
+  return launch_pt_loop<PCS_F_NULL>(a, n, b, st);
+}
+
+int64_t pcs_grid_bar_bytes(void) { return 512; }
 
 int64_t pcs_ctrl_bytes(void) { return 64; }
 

@@ -156,6 +156,12 @@ class PDS2DEngine:
         # host cost is far below the step, and back-to-back launches measured faster than
         # replaying a captured graph of the same launches; small images keep the graph
         self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
+        # PCS_PERSISTENT=1: a native chunk is ONE launch with a grid barrier per iteration
+        # (pcs_pds2d_run_persistent; pointwise-F family only, else the back-to-back launches)
+        self.persistent = self.native and os.environ.get('PCS_PERSISTENT', '0') == '1'
+        self.bar = None
+        if self.persistent:
+            self.bar = torch.zeros(int(self.lib.pcs_grid_bar_bytes()) // 4, dtype=torch.int32, device=dev)
 
     # one iteration with parity p (reads buffers p, writes 1-p)
     def _iteration(self, p, hist):
@@ -184,7 +190,18 @@ class PDS2DEngine:
         a.x, a.xn = self.X[0].data_ptr(), self.X[1].data_ptr()
         a.z, a.zn = self.Z[0].data_ptr(), self.Z[1].data_ptr()
         a.hist = hist.data_ptr()
+        if self.persistent:
+            rc = self.lib.pcs_pds2d_run_persistent(ctypes.byref(a), self.chunk, L.ptr(self.bar), L.stream())
+            if rc == 0:
+                return
+            if rc != -3:
+                L.check(rc, 'pcs_pds2d_run_persistent')
+            self.persistent = False  # not applicable to this problem
         L.check(self.lib.pcs_pds2d_run(ctypes.byref(a), self.chunk, L.stream()), 'pcs_pds2d_run')
+
+    def barrier_timed_out(self):
+        """True if a persistent launch's grid barrier gave up (grid not co-resident)."""
+        return self.bar is not None and int(self.bar[64].item()) != 0
 
     # ---- fixed-count loop for benchmarking (bench.py): no early stop, optional per-step events
     def prepare_fixed(self, total_iters, chunk):

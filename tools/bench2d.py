@@ -78,7 +78,8 @@ def run(name, pds, n, K, W):
     alg = 7 * n * n * 4
     print(json.dumps({'config': name, 'it_per_s': round(1e3 / ms, 1), 'us_per_iter': round(ms * 1e3, 2),
                       'alg_GBps': round(alg / (ms * 1e-3) / 1e9, 1), 'frac_of_8TBps': round(alg / (ms * 1e-3) / 8e12, 4),
-                      'native_launch': bool(eng.native), 'nblocks': eng.nblocks}), flush=True)
+                      'native_launch': bool(eng.native), 'persistent': bool(getattr(eng, 'persistent', False)),
+                      'nblocks': eng.nblocks}), flush=True)
 
 
 def main():
