@@ -311,6 +311,9 @@ static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hip
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_pt_loop<FK, HK>, 256, 0) != hipSuccess)
     return PCS_ELAUNCH;
   const int tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
+  // the occupancy query can over-report by one block/CU for SGPR-heavy kernels: at most 4
+  // blocks of 256 threads per CU for a grid that must be co-resident
+  nb = nb > 4 ? 4 : nb;
   if (tiles_x < 2 || nb < 1) return PCS_EUNSUPPORTED;
   MarchPlan p;  // one wave of this kernel's resident workgroups
   plan_bands(full_bands(a), PtGeom::TS, tiles_x, cus * nb, 4, &p);

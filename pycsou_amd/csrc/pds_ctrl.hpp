@@ -166,6 +166,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, int* 
     unsigned* gen = bar + 32;
     const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait can be dropped (ROCm 7.2)
     int ok = 1;
     if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1) {
       __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -182,6 +183,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, int* 
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // invalidate complete before the barrier
     flag[1] = ok && __hip_atomic_load(bar + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
   }
   __syncthreads();
