@@ -121,10 +121,12 @@ __device__ __forceinline__ G4<float> bload4(Rsrc r, uint32_t off) {
   return {{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])}};
 }
 // 16-B store through a descriptor: an offset carrying kOOB is dropped by the range check
+// AUX: cache-policy bits of the store (0 = plain; 16 = sc1, written through and dropped from L2)
+template <int AUX = 0>
 __device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, const G4<float>& g) {
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
   const u4 d = {__float_as_uint(g.v[0]), __float_as_uint(g.v[1]), __float_as_uint(g.v[2]), __float_as_uint(g.v[3])};
-  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)off, 0, AUX);
 }
 
 // One halo'd array: its descriptor, row pitch in bytes, and the local rows it can supply

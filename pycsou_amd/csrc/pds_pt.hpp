@@ -28,7 +28,7 @@ struct PtGeom {
   static constexpr int SZ = O_Z1 + SZ_Z1;
 };
 
-template <int FK, int HK>
+template <int FK, int HK, int SAUX = 0>
 __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __restrict__ xn,
                                         const float* __restrict__ z, float* __restrict__ zn,
                                         const float* __restrict__ gsrc, const Slab32& s, const Params<float>& P, int gk,
@@ -150,7 +150,7 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
     }
     st4(U + slot * WG + 4 * g, uo);
     if (g == TW / 4 - 1) U[slot * WG + TW] = ue;
-    bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+    bstore4<SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
   };
   // ---- P6: z' on row lr = a + ui
   auto p6 = [&](int a, int fl, int ub) {
@@ -197,8 +197,8 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
       part[3] += (double)sz;
     }
     const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_u;
-    bstore4(rzn0, off, o0);
-    bstore4(rzn1, off, o1);
+    bstore4<SAUX>(rzn0, off, o0);
+    bstore4<SAUX>(rzn1, off, o1);
   };
 
   // prologue: u on row s0 (step a = s0 - TS, row TS - 1 of its P45), x' on row s0
@@ -285,7 +285,9 @@ __global__ __launch_bounds__(256) void k_pds2d_pt_loop(float* x0, float* x1, flo
     if (flag[0] != 0) break;  // uniform: written before the last barrier (solver.py:65-66)
     const bool odd = i & 1;
     double part[4] = {0.0, 0.0, 0.0, 0.0};
-    pt_task<FK, HK>(odd ? x1 : x0, odd ? x0 : x1, odd ? z1 : z0, odd ? z0 : z1, gsrc, s, P, gk, s0, s1,
+    // sc1 stores: x'/z' leave the XCD's L2 as they are written, so the barrier's release
+    // has (almost) nothing dirty to write back
+    pt_task<FK, HK, 16>(odd ? x1 : x0, odd ? x0 : x1, odd ? z1 : z0, odd ? z0 : z1, gsrc, s, P, gk, s0, s1,
                     strip * PtGeom::TW, sm, part);
     block_sum<4>(part, red);
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
