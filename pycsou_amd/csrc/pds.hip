@@ -259,7 +259,12 @@ static int pt_slots() {
         nb < 1)
       nb = 4;
     (void)hipGetLastError();
-    slots = cus * nb;
+    // 3 workgroups per CU (fewer, longer row segments) although 5 fit: C2 2048^2 measured
+    // 29.9 us/iteration at 768 workgroups against 35.7 at 1024-2560 and 30.8 at 512
+    // (profiles/r1_c2_pt_grid_sweep.txt)
+    slots = cus * (nb < 3 ? nb : 3);
+    const char* e = getenv("PCS_PT_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
   }
   return slots;
 }
@@ -313,7 +318,7 @@ static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hip
   const int tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
   // the occupancy query can over-report by one block/CU for SGPR-heavy kernels: at most 4
   // blocks of 256 threads per CU for a grid that must be co-resident
-  nb = nb > 4 ? 4 : nb;
+  nb = nb > 3 ? 3 : nb;  // and 3 per CU is the fastest grid of the per-launch kernel too
   if (tiles_x < 2 || nb < 1) return PCS_EUNSUPPORTED;
   MarchPlan p;  // one wave of this kernel's resident workgroups
   plan_bands(full_bands(a), PtGeom::TS, tiles_x, cus * nb, 4, &p);
