@@ -790,6 +790,8 @@ static int sep_march_slots() {
       nb = 2;
     (void)hipGetLastError();
     slots = cus * nb;
+    const char* e = getenv("PCS_SEP2D_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
   }
   return slots;
 }
