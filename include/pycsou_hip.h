@@ -80,6 +80,24 @@ int pcs_lap_adj(int dtype, const void* y, void* out, const int64_t* dims, const 
  * and offsets (kh-1-off0, kw-1-off1). */
 int pcs_conv2d(int dtype, const void* x, void* out, int64_t n0, int64_t n1, const void* psf, int kh, int kw,
                int off0, int off1, const void* b, double beta, hipStream_t stream);
+/* x == out is rejected (PCS_EINVAL); b == out is allowed.  Odd square PSFs centred at
+ * (kh/2, kw/2) of size 3..15 or 31 run the register-blocked marching kernel (corr2d.hip);
+ * other shapes run the LDS-tiled kernel, or use the plan entry points below. */
+
+/* Convolve2D through a packed plan (same operator, any PSF up to 31 x 31): every call is
+ * one correlation with a K x K window centred at K/2, K = the "tier" (odd, 3..15 or 31)
+ * returned by pcs_conv2d_plan_tier (< 0: unsupported).  pcs_conv2d_plan_pack is a HOST
+ * function: it writes the forward (adjoint = 0) or adjoint (adjoint = 1) window of the
+ * fp64 host PSF into a host buffer of pcs_conv2d_plan_bytes bytes of `dtype`, which the
+ * caller copies to the device once.  pcs_conv2d_planned then computes
+ *   out = Conv(x) (+ beta * b)  (plan of adjoint = 0)  or  Conv^T(x) (+ beta * b)  (adjoint = 1)
+ * Same arithmetic as pcs_conv2d up to floating-point summation order.  x != out. */
+int pcs_conv2d_plan_tier(int kh, int kw, int off0, int off1);
+int64_t pcs_conv2d_plan_bytes(int dtype, int kh, int kw, int off0, int off1);
+int pcs_conv2d_plan_pack(int dtype, const double* psf, int kh, int kw, int off0, int off1, int adjoint,
+                         void* plan_host);
+int pcs_conv2d_planned(int dtype, const void* x, void* out, int64_t n0, int64_t n1, const void* plan, int tier,
+                       const void* b, double beta, hipStream_t stream);
 
 /* Convolve1D along `axis` of a 1..3-D array (pycsou/linop/conv.py:20-164 -> pylops Convolve1D):
  * out[i] = sum_t h[t] x[i + (off - t) e_axis].  Adjoint = flipped taps, off' = k-1-off. */

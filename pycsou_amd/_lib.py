@@ -78,6 +78,10 @@ _SIGS = {
     'pcs_lap_adj': (_c_int, [_c_int, _vp, _vp, _pi64, _pdbl, _pdbl, _c_int, _vp]),
     'pcs_conv2d': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_dbl,
                             _vp]),
+    'pcs_conv2d_plan_tier': (_c_int, [_c_int, _c_int, _c_int, _c_int]),
+    'pcs_conv2d_plan_bytes': (_c_i64, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    'pcs_conv2d_plan_pack': (_c_int, [_c_int, _pdbl, _c_int, _c_int, _c_int, _c_int, _c_int, _vp]),
+    'pcs_conv2d_planned': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _vp, _c_int, _vp, _c_dbl, _vp]),
     'pcs_conv1d': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _vp, _c_int, _c_int, _vp]),
     'pcs_conv2d_sep_planes': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_int, _c_int, _vp, _c_int,
                                         _c_int, _c_int, _vp]),

@@ -282,6 +282,32 @@ def conv2d(x, dims, psf_dev, kh, kw, off0, off1, b=None, beta=0.0):
     return out
 
 
+def conv2d_plan(psf, off0, off1, adjoint, dtype):
+    """Packed correlation window of a PSF for pcs_conv2d_planned (host pack, one device copy):
+    returns (tier, device tensor) or None if the PSF is larger than the kernel's tiers."""
+    lib = L.load()
+    h = np.ascontiguousarray(np.asarray(psf, dtype=np.float64))
+    kh, kw = h.shape
+    tier = int(lib.pcs_conv2d_plan_tier(kh, kw, int(off0), int(off1)))
+    if tier < 0:
+        return None
+    code = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+    nbytes = int(lib.pcs_conv2d_plan_bytes(code, kh, kw, int(off0), int(off1)))
+    host = np.empty(nbytes // (4 if code == L.PCS_F32 else 8), dtype=np.float32 if code == L.PCS_F32 else np.float64)
+    L.check(lib.pcs_conv2d_plan_pack(code, h.ctypes.data_as(L._pdbl), kh, kw, int(off0), int(off1), int(adjoint),
+                                     host.ctypes.data), 'pcs_conv2d_plan_pack')
+    return tier, torch.as_tensor(host).to(device=device())
+
+
+def conv2d_planned(x, dims, plan, b=None, beta=0.0, out=None):
+    lib = L.gpu()
+    tier, w = plan
+    out = torch.empty_like(x) if out is None else out
+    L.check(lib.pcs_conv2d_planned(L.dtcode(x), L.ptr(x), L.ptr(out), int(dims[0]), int(dims[1]), L.ptr(w), int(tier),
+                                   L.ptr(b), float(beta), L.stream()), 'pcs_conv2d_planned')
+    return out
+
+
 def conv1d(x, dims, axis, taps_dev, k, off):
     lib = L.gpu()
     out = torch.empty_like(x)

@@ -927,6 +927,9 @@ static int conv1d(const void* x, void* out, int ndim, const int64_t* dims, int a
   return launch_status();
 }
 
+int corr2d_raw(int dt, const void* x, void* out, int64_t n0, int64_t n1, const void* psf, int kh, int kw, int off0,
+               int off1, const void* b, double beta, hipStream_t st);  // corr2d.hip
+
 }  // namespace pcs
 
 using namespace pcs;
@@ -935,6 +938,12 @@ extern "C" {
 
 int pcs_conv2d(int dt, const void* x, void* out, int64_t n0, int64_t n1, const void* psf, int kh, int kw, int off0,
                int off1, const void* b, double beta, hipStream_t st) {
+  if (x && x == out) return PCS_EINVAL;  // the stencil reads neighbours of every output
+  if ((dt == PCS_F32 || dt == PCS_F64) && x && out && psf) {
+    // odd square centred PSFs (3..15, 31): the register-blocked marching kernel (corr2d.hip)
+    const int rc = corr2d_raw(dt, x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
+    if (rc != PCS_EUNSUPPORTED) return rc;
+  }
   if (dt == PCS_F32) return conv2d<float>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
   if (dt == PCS_F64) return conv2d<double>(x, out, n0, n1, psf, kh, kw, off0, off1, b, beta, st);
   return PCS_EINVAL;

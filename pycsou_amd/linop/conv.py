@@ -5,8 +5,10 @@
 offset rule (``K//2`` for odd, ``K//2 - 1`` for even filters, ``conv.py:159-162,
 285-292``) and PyLops 1.x semantics: forward = zero-boundary 'same' convolution,
 adjoint = correlation.  The reference goes through ``scipy.signal.convolve(method='fft')``;
-here both directions are direct LDS-tiled gfx950 kernels (``pcs_conv2d`` /
-``pcs_conv1d``), identical up to floating-point rounding.
+here both directions are direct gfx950 kernels, identical up to floating-point rounding:
+``Convolve2D`` through a packed correlation plan (``pcs_conv2d_planned``, the register-blocked
+row-marching kernel of ``csrc/corr2d.hip``, PSFs up to 31 x 31; ``pcs_conv2d`` beyond),
+``Convolve1D`` through ``pcs_conv1d``.
 
 ``Convolve2D.separable()`` exposes a rank-1 factorisation ``h = c r^T`` when the PSF has
 one (a Gaussian PSF does to ~1e-16): the fused PDS engine then applies the blur as two
@@ -52,15 +54,32 @@ class Convolve2DOp(LinearOperator):
         self.off = (pycsou_offset(self.kh), pycsou_offset(self.kw))
         self._h = _DevCache(filt)
         self._hf = _DevCache(filt[::-1, ::-1])
+        self._plans = {}
+
+    def plan(self, dtype, adjoint):
+        """(tier, packed window) for pcs_conv2d_planned, or None (PSF wider than 31)."""
+        key = (dtype, bool(adjoint))
+        if key not in self._plans:
+            self._plans[key] = O.conv2d_plan(self.filter, self.off[0], self.off[1], adjoint, dtype)
+        return self._plans[key]
 
     def _apply(self, t):
+        p = self.plan(t.dtype, False)
+        if p is not None:
+            return O.conv2d_planned(t, self.dims, p)
         return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off)
 
     def _apply_minus(self, t, y):
         """Conv x - y in one kernel (residual of the data-fidelity term)."""
+        p = self.plan(t.dtype, False)
+        if p is not None:
+            return O.conv2d_planned(t, self.dims, p, b=y, beta=-1.0)
         return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off, b=y, beta=-1.0)
 
     def _adj(self, t):
+        p = self.plan(t.dtype, True)
+        if p is not None:
+            return O.conv2d_planned(t, self.dims, p)
         return O.conv2d(t, self.dims, self._hf.get(t.dtype), self.kh, self.kw, self.kh - 1 - self.off[0],
                         self.kw - 1 - self.off[1])
 

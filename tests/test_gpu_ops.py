@@ -104,6 +104,78 @@ def test_convolve2d(A, dtype, kshape, shape):
     assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
 
 
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('k', [3, 5, 7, 9, 11, 13, 15, 31])
+@pytest.mark.parametrize('shape', [(64, 64), (37, 130), (300, 7), (1, 1)])
+def test_conv2d_raw_tiers(A, dtype, k, shape):
+    """pcs_conv2d with an odd square centred PSF runs the marching correlation kernel with the
+    PSF read flipped (forward) -- and its adjoint call (flipped PSF, mirrored offset); with the
+    fused residual out = h*x - y."""
+    from pycsou_amd import _lib as L
+    lib = L.gpu()
+    rng = np.random.default_rng(k)
+    h = rng.standard_normal((k, k))
+    N = shape[0] * shape[1]
+    x = rng.standard_normal(N).astype(dtype)
+    y = rng.standard_normal(N).astype(dtype)
+    ref = P.Convolve2D(N, h, shape, offset=(k // 2, k // 2), method='direct')
+    xd, yd, hd, hfd = dev(x), dev(y), dev(h.astype(dtype)), dev(h[::-1, ::-1].astype(dtype))
+    out = torch.empty_like(xd)
+    code = L.dtcode(xd)
+    assert lib.pcs_conv2d(code, L.ptr(xd), L.ptr(out), shape[0], shape[1], L.ptr(hd), k, k, k // 2, k // 2, L.ptr(yd),
+                          -1.0, L.stream()) == 0
+    assert rel(host(out), ref.matvec(x.astype(np.float64)) - y) < 10 * TOL[dtype]
+    assert lib.pcs_conv2d(code, L.ptr(xd), L.ptr(out), shape[0], shape[1], L.ptr(hfd), k, k, k // 2, k // 2, None,
+                          0.0, L.stream()) == 0
+    assert rel(host(out), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('kshape', [(15, 15), (6, 11), (1, 30)])
+@pytest.mark.parametrize('shape', [(1000, 4096), (517, 1023), (130, 64)])
+def test_conv2d_planned_large(A, dtype, kshape, shape):
+    """Packed-plan Convolve2D (pcs_conv2d_planned) at ragged and large sizes (many strip
+    segments, partial last marching blocks, widths that are not 16-B multiples), forward,
+    adjoint and the fused residual h*x - y, against the direct oracle."""
+    from pycsou_amd.linop.conv import Convolve2D
+    rng = np.random.default_rng(7)
+    h = rng.standard_normal(kshape)
+    N = shape[0] * shape[1]
+    x = rng.standard_normal(N).astype(dtype)
+    y = rng.standard_normal(N).astype(dtype)
+    off = tuple(P.pycsou_offset(n) for n in kshape)
+    ref = P.Convolve2D(N, h, shape, offset=off, method='fft')
+    op = Convolve2D(N, h, shape)
+    assert op.plan(torch.float32 if dtype == np.float32 else torch.float64, False) is not None
+    xd, yd = dev(x), dev(y)
+    x64 = x.astype(np.float64)
+    tol = 10 * TOL[dtype] if dtype == np.float32 else 1e-11  # the oracle is SciPy FFT here
+    assert rel(host(op._apply(xd)), ref.matvec(x64)) < tol
+    assert rel(host(op._adj(xd)), ref.rmatvec(x64)) < tol
+    assert rel(host(op._apply_minus(xd, yd)), ref.matvec(x64) - y) < tol
+
+
+def test_conv2d_plan_pack(A):
+    """Host packing: forward window = flipped zero-padded PSF centred at K/2, adjoint window =
+    the padded PSF; tier choice and rejection of PSFs wider than 31."""
+    from pycsou_amd import _lib as L
+    lib = L.load()
+    h = np.arange(1, 7, dtype=np.float64).reshape(2, 3)  # off = (0, 1)
+    assert lib.pcs_conv2d_plan_tier(2, 3, 0, 1) == 3
+    assert lib.pcs_conv2d_plan_tier(40, 3, 19, 1) == -3
+    assert lib.pcs_conv2d_plan_tier(2, 3, 2, 1) == -1
+    nb = lib.pcs_conv2d_plan_bytes(1, 2, 3, 0, 1)
+    assert nb == 3 * 16 * 8
+    for adj in (0, 1):
+        buf = np.full(nb // 8, np.nan)
+        assert lib.pcs_conv2d_plan_pack(1, h.ctypes.data_as(L._pdbl), 2, 3, 0, 1, adj, buf.ctypes.data) == 0
+        wmat = buf.reshape(3, 16)
+        assert np.all(wmat[:, 3:] == 0)
+        hp = np.zeros((3, 3))
+        hp[1:3, 0:3] = h  # h'[i + s0][j + s1], s0 = 1 - 0, s1 = 1 - 1
+        np.testing.assert_array_equal(wmat[:, :3], hp if adj else hp[::-1, ::-1])
+
+
 def test_convolve2d_doctest(A):
     from pycsou_amd.linop.conv import Convolve2D
     f = load('ops.npz')
