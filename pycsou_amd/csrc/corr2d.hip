@@ -31,6 +31,26 @@
 // their halo columns in one XCD's L2).
 #include "common.hpp"
 
+// diagnostics variants (PCS_LIB_PATH builds, tools/conv2d_bench.py): register prefetch of the
+// next block's rows (PRE).  Measured on 4096^2 fp32 (r2 session): SGPR taps (scalar loads),
+// single-buffered input rows, 3-4 waves/SIMD register budgets and a one-burst read schedule
+// were all equal or slower than this configuration (96.5-116 us against 97-98 us for k = 15).
+#ifndef PCS_CORR_PRE
+#define PCS_CORR_PRE 1
+#endif
+// spread the next row's LDS reads through the current row's FMAs (sched_group_barrier)
+// instead of issuing them as one burst ahead of the FMAs
+#ifndef PCS_CORR_SPREAD
+#define PCS_CORR_SPREAD 1
+#endif
+#ifndef PCS_CORR_SPREAD_DIV
+#define PCS_CORR_SPREAD_DIV 2
+#endif
+// ablations (timing only, wrong results): 1 = no FMAs, 2 = no ring fill
+#ifndef PCS_CORR_ABLATE
+#define PCS_CORR_ABLATE 0
+#endif
+
 namespace pcs {
 
 namespace corr2d {
@@ -166,9 +186,10 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
       }
     }
   };
-  issue(0);
+  if (PCS_CORR_PRE && PCS_CORR_ABLATE != 2) issue(0);
 
   for (int blk = 0; blk < nblk; ++blk) {
+    if (!PCS_CORR_PRE && PCS_CORR_ABLATE != 2) issue(blk);
     {  // land the prefetched rows: window rows blk*TH + K-1 + rr -> ring slot mod RS
       const int s0 = (int)(((int64_t)blk * TH + (K - 1)) % RS);
 #pragma unroll
@@ -183,7 +204,7 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
       }
     }
     lds_barrier();
-    if (blk + 1 < nblk) issue(blk + 1);
+    if (PCS_CORR_PRE && PCS_CORR_ABLATE != 2 && blk + 1 < nblk) issue(blk + 1);
 
     const int64_t g = r0 + (int64_t)blk * TH + trow;  // this thread's output row
     // a wave whose 16 rows all lie past the segment skips the arithmetic
@@ -202,6 +223,10 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
         }
       };
       auto fmas = [&](const T (&in)[WIN], const T (&h)[KP]) {
+        if (PCS_CORR_ABLATE == 1) {
+          acc[0] += in[LEFT] * h[0];
+          return;
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j)
 #pragma unroll
@@ -226,18 +251,28 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
       rd(ia, s);
       rdt(ha, 0);
       // two window rows per trip, the next row's inputs and taps read while the current row's
-      // FMAs run (K odd: the last row after the loop)
+      // FMAs run (K odd: the last row after the loop).  spread() pins the schedule: left alone,
+      // the machine scheduler sinks the prefetch reads to just before their use, so the next
+      // row's LDS latency would not overlap this row's FMAs.
 #pragma unroll 1
       for (int q = 0; q < K - 1; q += 2) {
+        // everything this half consumes was requested a half-step ago: wait for it before
+        // requesting the next row, so no wait inside the FMAs covers the fresh requests
+        __builtin_amdgcn_s_waitcnt(0xC07F);
         if (++s == RS) s = 0;
         rd(ib, s);
         rdt(hb, q + 1);
+        if (!PCS_CORR_SPREAD) __builtin_amdgcn_sched_barrier(0);
         fmas(ia, ha);
+        spread();
         keep(ib);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
         if (++s == RS) s = 0;
         rd(ia, s);
         rdt(ha, q + 2);
+        if (!PCS_CORR_SPREAD) __builtin_amdgcn_sched_barrier(0);
         fmas(ib, hb);
+        spread();
         keep(ia);
       }
       fmas(ia, ha);

@@ -7,7 +7,7 @@ for path in sys.argv[1:]:
             k = r['Kernel_Name'][:60]
             vals[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k, d in vals.items():
-    if 'k_pds2d' not in k and 'reduce' not in k and 'conv' not in k and 'grad' not in k:
+    if not any(t in k for t in ('k_pds', 'reduce', 'conv', 'grad', 'corr', 'sep2d')):
         continue
     print(k)
     for c, v in sorted(d.items()):
