@@ -247,6 +247,21 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
         for (int t = 0; t < KP / V; ++t)
           *reinterpret_cast<corr2d::u32x4*>(dst + t * V) = *reinterpret_cast<const corr2d::u32x4*>(p + t * V);
       };
+      // one LDS read, then GV FMAs, NR times (NR = the step's reads), over the first half of
+      // this row's FMAs: the reads for the next row stream beside them and the second half
+      // covers their latency
+      auto spread = [&]() {
+        constexpr int NR = NB + KP / V;
+        constexpr int GV = C * K / (PCS_CORR_SPREAD_DIV * NR);
+        if (PCS_CORR_SPREAD) {
+#pragma unroll
+          for (int t = 0; t < NR; ++t) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x002, GV, 0);  // VALU
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
       T ia[WIN], ib[WIN], ha[KP], hb[KP];
       rd(ia, s);
       rdt(ha, 0);
