@@ -22,6 +22,14 @@ schedule (halo exchange and sums all-gather overlapped with the interior planes)
 after the C3 measurement under a watchdog: if it fails or stalls, the C3 line is printed
 without it.
 
+Single-GPU 2-D legs in the same line (`c2`: BASELINE configs[1], 2048^2 fp32 TV denoising;
+`c3_nonsep`: the C3 problem with a non-separable 15x15 PSF through the register-blocked
+correlation kernel), each with its own roofline.  The operator norms of the single-GPU 2-D
+problems come from compute_lipschitz_cst() (device Lanczos, untimed setup) as in a reference
+script; the multi-GPU and volume problems use the closed forms (documented in the line).
+
+Counts: exactly --warmup untimed and --steps timed iterations (odd counts allowed).
+
 Prints ONE JSON line on rank 0.
 """
 
@@ -58,8 +66,22 @@ def gaussian_psf(size=15, sigma=2.0):
     return h / h.sum()
 
 
-def build_problem(n0, n1, dtype, seed=0):
-    """The C3 problem through the public API (pycsou scripts look exactly like this)."""
+def aniso_psf(size=15, su=3.0, sv=1.2, angle=np.pi / 6):
+    """Rotated anisotropic Gaussian (nonnegative, unit sum, rank > 1): the non-separable PSF of
+    the c3_nonsep leg."""
+    r = np.arange(size) - (size - 1) / 2
+    yy, xx = np.meshgrid(r, r, indexing='ij')
+    u = np.cos(angle) * xx + np.sin(angle) * yy
+    v = -np.sin(angle) * xx + np.cos(angle) * yy
+    h = np.exp(-0.5 * ((u / su) ** 2 + (v / sv) ** 2))
+    return h / h.sum()
+
+
+def build_problem(n0, n1, dtype, seed=0, psf=None, lipschitz='lanczos'):
+    """The C3 problem through the public API (pycsou scripts look exactly like this).
+    lipschitz='lanczos': K.compute_lipschitz_cst() / C.compute_lipschitz_cst() as a reference
+    script does (device Lanczos, untimed setup); 'analytic': the closed forms (||grad_fwd|| from
+    the Neumann-Laplacian spectrum, ||C|| <= 1 for a nonnegative unit-sum PSF)."""
     from pycsou_amd.func.loss import SquaredL2Loss
     from pycsou_amd.func.penalty import L21Norm
     from pycsou_amd.linop.conv import Convolve2D
@@ -67,16 +89,42 @@ def build_problem(n0, n1, dtype, seed=0):
     from pycsou_amd.opt.proxalgs import PDS
     N = n0 * n1
     xs = torch.as_tensor(phantom((n0, n1), 64, seed).ravel()).to('cuda', dtype)
-    C = Convolve2D(size=N, filter=gaussian_psf(15, 2.0), shape=(n0, n1))
-    C.lipschitz_cst = C.diff_lipschitz_cst = 1.0  # nonnegative PSF of unit sum: ||Conv|| <= 1
+    C = Convolve2D(size=N, filter=gaussian_psf(15, 2.0) if psf is None else psf, shape=(n0, n1))
+    K = Gradient(shape=(n0, n1), kind='forward')
+    if lipschitz == 'lanczos':
+        C.compute_lipschitz_cst()
+        K.compute_lipschitz_cst()
+    else:
+        C.lipschitz_cst = C.diff_lipschitz_cst = 1.0  # nonnegative PSF of unit sum: ||Conv|| <= 1
+        # exact ||grad_fwd|| on an n0 x n1 grid (eigenvalues of the Neumann Laplacian)
+        K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(4 * np.sin(np.pi * (n0 - 1) / (2 * n0)) ** 2
+                                                                + 4 * np.sin(np.pi * (n1 - 1) / (2 * n1)) ** 2))
     g = torch.Generator(device='cuda').manual_seed(seed + 1)
     y = C(xs) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
-    K = Gradient(shape=(n0, n1), kind='forward')
-    # exact ||grad_fwd|| on an n0 x n1 grid (eigenvalues of the Neumann Laplacian)
-    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(4 * np.sin(np.pi * (n0 - 1) / (2 * n0)) ** 2
-                                                            + 4 * np.sin(np.pi * (n1 - 1) / (2 * n1)) ** 2))
     F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
     H = 0.05 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2))
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+               z0=torch.zeros(2 * N, dtype=dtype, device='cuda'), verbose=None)
+
+
+def build_denoise(n, dtype, seed=0, lipschitz='lanczos'):
+    """C2 (BASELINE configs[1]): 2-D TV denoising n x n, F = 1/2 ||x - y||^2, K = Gradient(forward),
+    H = 0.1 * L21Norm (isotropic TV), fp32."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    N = n * n
+    xs = torch.as_tensor(phantom((n, n), 64, seed).ravel()).to('cuda', dtype)
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = xs + 0.1 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
+    K = Gradient(shape=(n, n), kind='forward')
+    if lipschitz == 'lanczos':
+        K.compute_lipschitz_cst()
+    else:
+        K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(8 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y)
+    H = 0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2))
     return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
                z0=torch.zeros(2 * N, dtype=dtype, device='cuda'), verbose=None)
 
@@ -213,11 +261,106 @@ def spin_up(eng, n_launch, min_ms=60.0):
         busy += n_launch * eng.time_step_kernel(n_launch)
 
 
+def spin_up_fixed(eng, min_ms=60.0):
+    """spin_up for a prepare_fixed() engine: whole iterations (every kernel of one) until the
+    GPU has been busy >= min_ms; the caller re-prepares the loop state afterwards."""
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < min_ms:
+        eng.advance_fixed(10)
+        torch.cuda.synchronize()
+
+
+def fused_2d(pds, dtype, K, W, chunk=32):
+    """Exactly W untimed then K timed iterations of a fused 2-D problem (PDS2DEngine, fixed
+    count); HIP events on the launch stream bracket the K iterations.  Returns ms per
+    iteration, the isolated per-kernel launch means and the engine facts."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    spec = pds._fused_spec()
+    assert spec is not None, 'problem must take the fused 2-D engine'
+    eng = PDS2DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    total = W + K + 4
+    eng.prepare_fixed(total, chunk)
+    spin_up_fixed(eng)
+    eng.prepare_fixed(total, chunk)  # fresh loop state: exactly W + K iterations below
+    eng.advance_fixed(W)
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    eng.advance_fixed(K)
+    t1.record()
+    torch.cuda.synchronize()
+    ms = t0.elapsed_time(t1) / K
+    it_done = int(eng.ctrl.view(torch.int32)[0].item())
+    assert it_done == W + K, (it_done, W, K)  # every timed launch really iterated
+    # per-kernel means: an event pair around each launch of 100 eager iterations (after the
+    # timed region; the rocprofv3 kernel-trace averages in profiles/ must agree)
+    kern = eng.time_iteration_kernels(min(max(K, 20), 100))
+    res = {'ms_per_step': ms, 'kernels_ms': kern, 'nblocks': eng.nblocks, 'native': eng.native,
+           'fkind': int(eng.fkind)}
+    del eng
+    torch.cuda.empty_cache()
+    return res
+
+
+def leg_c2(args, dtype, K, W):
+    """C2 (BASELINE configs[1]) 2048^2 fp32 TV denoising: it/s and the step kernel against the
+    HBM roofline (7 N words per iteration)."""
+    n = 2048
+    pds = build_denoise(n, dtype, lipschitz=args.lipschitz)
+    r = fused_2d(pds, dtype, K, W)
+    del pds
+    elem = 4 if dtype == torch.float32 else 8
+    alg = 7 * n * n * elem
+    km = r['kernels_ms']['step']
+    return {'workload': f'C2 TV denoising {n}x{n} {args.dtype}, Gradient(kind=forward), 0.1*L21Norm, '
+                        f'PDS fused step (pcs_pds2d_step, row-marching pointwise-F kernel)',
+            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg,
+            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'roofline': {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_pt<DENOISE,L21>)', 'kernel_ms': round(km, 5),
+                         'achieved': round(alg / (km * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def leg_c3_nonsep(args, dtype, K, W):
+    """The C3 problem with a NON-separable 15x15 PSF (rotated anisotropic Gaussian, rank > 1):
+    per iteration r = h*x - y and g = h^T r by the register-blocked correlation kernel
+    (pcs_conv2d_planned, fp32-vector bound: 2 x 225 FMA per pixel), then the fused update
+    with grad F read from g (pcs_pds2d_step, GRADBUF); the three launches per iteration are
+    replayed from a captured hipGraph."""
+    n = args.size
+    pds = build_problem(n, n, dtype, psf=aniso_psf(), lipschitz=args.lipschitz)
+    r = fused_2d(pds, dtype, K, W)
+    del pds
+    elem = 4 if dtype == torch.float32 else 8
+    N = n * n
+    alg = 7 * N * elem
+    km = r['kernels_ms']
+    conv_flop = 2 * 225 * N  # one pass: 225 FMA per pixel
+    conv_ms = 0.5 * (km['conv_fwd'] + km['conv_adj'])
+    return {'workload': f'C3 TV-deconvolution {n}x{n} {args.dtype}, NON-separable 15x15 PSF (rotated '
+                        f'anisotropic Gaussian 3.0/1.2 px, 30 deg, rank > 1), Gradient(kind=forward), 0.05*L21Norm; '
+                        f'conv r = h*x - y, g = h^T r (pcs_conv2d_planned x2) + fused update (GRADBUF), hipGraph-replayed',
+            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+            'steps': K, 'warmup': W, 'kernels_ms': {k: round(v, 5) for k, v in km.items()},
+            'alg_bytes_per_iter': alg,
+            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'roofline': {'bound': 'fp32-vector', 'kernel': 'pcs_conv2d_planned (k_corr2d<float,15>)',
+                         'kernel_ms': round(conv_ms, 5), 'achieved': round(conv_flop / (conv_ms * 1e-3) / 1e12, 2),
+                         'peak': 157.3, 'unit': 'TFLOP/s',
+                         'frac': round(conv_flop / (conv_ms * 1e-3) / 1e12 / 157.3, 4),
+                         'flop_per_launch': conv_flop},
+            'update_roofline': {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_pt<GRADBUF,L21>)',
+                                'kernel_ms': round(km['step'], 5),
+                                'achieved': round(alg / (km['step'] * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                                'unit': 'GB/s', 'frac': round(alg / (km['step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
 def slab_bench(n, dtype, K, W, world):
     """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
     (barrier + synchronize on both sides; the caller takes the max over ranks)."""
     from pycsou_amd.parallel import DistComm, SlabPDS2D
-    pds = build_problem(n * world, n, dtype)
+    pds = build_problem(n * world, n, dtype, lipschitz='analytic')
     comm = DistComm() if world > 1 else None
     kw = dict(rank=0 if comm is None else None, world=1 if comm is None else None)
     try:  # the native loop (RCCL bound by the library) unless it cannot be set up on this box
@@ -268,6 +411,11 @@ def main():
     ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
                     help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
+    ap.add_argument('--legs', default='c2,c3_nonsep',
+                    help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
+                         'PSF); "" skips them')
+    ap.add_argument('--lipschitz', default='lanczos', choices=['lanczos', 'analytic'],
+                    help='operator norms of the single-GPU 2-D problems: compute_lipschitz_cst() or closed forms')
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
                     help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
     args = ap.parse_args()
@@ -288,42 +436,24 @@ def main():
             dist.init_process_group(backend)
     dtype = torch.float32 if args.dtype == 'f32' else torch.float64
     n = args.size
-    K = max(2, args.steps + (args.steps % 2))
-    W = max(0, args.warmup + (args.warmup % 2))
-    # iterations per chunk: the largest even divisor of both K and W (<= 50)
-    chunk = max(c for c in range(2, min(K, 50) + 1, 2) if K % c == 0 and W % c == 0)
+    K = max(1, args.steps)  # exactly the requested counts (odd counts run a single trailing launch)
+    W = max(0, args.warmup)
 
     out = None
     if world > 1 or args.engine == 'slab':
         res = slab_bench(n, dtype, K, W, world)
+        res['kernel_ms_isolated'] = res['kernel_ms']
     else:
-        pds = build_problem(n, n, dtype)
-        from pycsou_amd.opt.engine import PDS2DEngine
+        pds = build_problem(n, n, dtype, lipschitz=args.lipschitz)
+        lips = {'K': pds.K.lipschitz_cst, 'Conv': pds.F.map2.lipschitz_cst}
         spec = pds._fused_spec()
         assert spec is not None and spec['fkind'] == 2, 'C3 problem must take the fused separable engine'
-        eng = PDS2DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
-        eng.prepare_fixed(W + K + 4, chunk)
-        spin_up(eng, min(K, 50))
-        eng.prepare_fixed(W + K + 4, chunk)  # fresh loop state: exactly W + K iterations below
-        for _ in range(W // chunk):
-            eng.replay()
-        torch.cuda.synchronize()
-        t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t_start.record()
-        for _ in range(K // chunk):
-            eng.replay()
-        t_end.record()
-        torch.cuda.synchronize()
-        ms = t_start.elapsed_time(t_end) / K
-        it_done = int(eng.ctrl.view(torch.int32)[0].item())
-        assert it_done == W + K, (it_done, W, K)  # every timed launch really iterated
-        # one launch of the step kernel per step: its average duration over the timed region
-        # (HIP events on its stream, inter-launch gaps included) is ms; the isolated per-launch
-        # figure (an event pair around each of 100 eager launches) is reported beside it
-        res = {'ms_per_step': ms, 'kernel_ms': ms, 'kernel_ms_isolated': eng.time_step_kernel(min(K, 100)),
-               'nblocks': eng.nblocks}
-        del eng, pds
-        torch.cuda.empty_cache()
+        res = fused_2d(pds, dtype, K, W)
+        del pds
+        # the step kernel's mean duration: an event pair around each of 100 isolated launches
+        # (rocprofv3 kernel-trace average in profiles/ agrees); ms_per_step is the whole loop
+        res['kernel_ms'] = res['kernel_ms_isolated'] = res['kernels_ms']['step']
+        res['lipschitz'] = lips
 
     if rank == 0:
         elem = 4 if dtype == torch.float32 else 8
@@ -344,18 +474,22 @@ def main():
             'config': {'workload': f'C3 TV-deconvolution {n}x{n} per GPU ({n * world}x{n} global, row slabs), '
                                    f'15x15 Gaussian PSF sigma=2 (rank-1: separable passes), isotropic TV '
                                    f'0.05*L21Norm, Gradient(kind=forward), PDS fused step, '
-                                   + (f'chunks of {chunk} iterations launched from C (pcs_pds2d_run)'
+                                   + ('iterations launched back to back from C (pcs_pds2d_run)'
                                       if 'nblocks' in res and world == 1
                                       and args.engine != 'slab' else
                                       f'slab engine ({res.get("loop", "python")} loop): per-iteration RCCL '
                                       f'all-gather of 4 sums + neighbour halo exchange'),
                        'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single',
-                       'schedule_trial_ms_serial_overlap': res.get('schedule_trial_ms')},
+                       'schedule_trial_ms_serial_overlap': res.get('schedule_trial_ms'),
+                       'lipschitz': args.lipschitz if world == 1 else 'analytic',
+                       'lipschitz_csts': res.get('lipschitz')},
+            'steps_requested': args.steps, 'warmup_requested': args.warmup,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,
                          'kernel': 'pcs_pds2d_step (k_pds2d_march<float,7,L21,256>)',
                          'kernel_ms': round(res['kernel_ms'], 5),
-                         'kernel_ms_isolated': round(res['kernel_ms_isolated'], 5), 'alg_bytes_per_launch': alg_bytes,
+                         'kernel_ms_source': 'mean of HIP-event pairs around each of 100 isolated launches',
+                         'alg_bytes_per_launch': alg_bytes,
                          # the 15x15 PSF work beside the bandwidth figure -- the separable
                          # passes (2 x 15 taps forward, 2 x 15 adjoint, 2 flop each) per pixel
                          'conv_flop_per_launch': 120 * N,
@@ -367,6 +501,14 @@ def main():
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:
             out['cpu_baseline'] = None
+        if world == 1 and args.engine != 'slab':
+            for leg in filter(None, args.legs.split(',')):
+                fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep}[leg]
+                try:
+                    out[leg] = fn(args, dtype, K, W)
+                except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
+                    out[leg] = {'error': f'{type(e).__name__}: {e}'[:300]}
+                    print(f'bench: leg {leg} failed: {out[leg]["error"]}', file=sys.stderr)
     for leg in filter(None, args.volumes.split(',')):
         name, edge, vdt, vsteps = leg.split(':')
         out = volume_leg(args, out if rank == 0 else None, f'volume_{name}', int(edge),

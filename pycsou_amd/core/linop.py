@@ -8,8 +8,8 @@ algebra (``linop.py:442-553``).  Subclasses implement the device-level ``_apply`
 
 ``compute_lipschitz_cst`` replaces ARPACK ``svds``/``eigsh`` (``linop.py:279-321``,
 host loop of tens to hundreds of operator applications) by a device Lanczos iteration
-on ``K^T K`` with full re-orthogonalisation: every operator application stays on the
-GPU, only the small tridiagonal eigenproblem runs on the host.
+on ``K^T K`` in O(1) vectors: every operator application and the recurrence stay on the
+GPU, only the small tridiagonal eigenproblem runs on the host every few steps.
 """
 
 from numbers import Number
@@ -21,34 +21,46 @@ from .. import _ops as O
 from .map import DifferentiableMap, DiffMapComp, DiffMapSum, Map, MapComp, MapSum
 
 
-def _lanczos_sigma_max(apply_gram, n, dtype, sym=False, tol=1e-10, max_steps=300, seed=0):
-    """Largest eigenvalue of the PSD Gram operator (or |eig| of a symmetric operator)
-    by Lanczos with full re-orthogonalisation; returns the eigenvalue estimate."""
+def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=10, seed=0):
+    """Largest eigenvalue of a PSD Gram operator (or largest |eigenvalue| of a symmetric one) by
+    plain Lanczos in fp64 with O(1) memory: three vectors of ``n`` (q_prev, q, w) plus what
+    ``apply`` allocates, no re-orthogonalisation (the extreme Ritz value converges regardless;
+    lost orthogonality only duplicates it).  The recurrence coefficients stay on the device
+    (no host sync per step); every ``check_every`` steps the tridiagonal matrix is copied to
+    the host and its extreme eigenvalue computed; the run stops when it moved by at most
+    ``tol`` (relative) since the previous check, or on an invariant subspace (beta ~ 0).
+    Ritz values never exceed the true extreme eigenvalue (up to rounding)."""
+    from scipy.linalg import eigvalsh_tridiagonal
+    dev = O.device()
     g = torch.Generator(device='cpu').manual_seed(seed)
-    q = torch.randn(n, generator=g, dtype=torch.float64).to(device=O.device(), dtype=dtype)
-    q = q / torch.linalg.vector_norm(q)
-    Q = torch.empty((min(max_steps, n) + 1, n), dtype=dtype, device=q.device)
-    Q[0] = q
-    alphas, betas = [], []
-    prev = None
-    theta = 0.0
-    for j in range(min(max_steps, n)):
-        w = apply_gram(Q[j])
-        a = float(torch.dot(w.double(), Q[j].double()))
-        alphas.append(a)
-        # full re-orthogonalisation (twice is enough)
-        for _ in range(2):
-            c = Q[:j + 1] @ w
-            w = w - Q[:j + 1].T @ c
-        b = float(torch.linalg.vector_norm(w.double()))
-        T = np.diag(alphas) + np.diag(betas, 1) + np.diag(betas, -1)
-        ev = np.linalg.eigvalsh(T)
+    q = torch.randn(n, generator=g, dtype=torch.float64).to(dev)
+    q /= torch.linalg.vector_norm(q)
+    q_prev = torch.zeros_like(q)
+    steps = max(1, min(int(max_steps), 10 * n + 10))
+    alphas = torch.zeros(steps, dtype=torch.float64, device=dev)
+    betas = torch.zeros(steps, dtype=torch.float64, device=dev)
+    b_prev = torch.zeros((), dtype=torch.float64, device=dev)
+    theta, prev = 0.0, None
+    for j in range(steps):
+        w = apply(q).to(torch.float64)
+        a = torch.dot(w, q)
+        w -= a * q
+        w -= b_prev * q_prev
+        b = torch.linalg.vector_norm(w)
+        alphas[j], betas[j] = a, b
+        q_prev, q, b_prev = q, w / b, b
+        if (j + 1) % check_every and j + 1 < steps:
+            continue
+        al = alphas[:j + 1].cpu().numpy()
+        be = betas[:j + 1].cpu().numpy()
+        scale = max(np.max(np.abs(al[np.isfinite(al)]), initial=0.0), 1e-300)
+        bad = np.nonzero(~np.isfinite(be) | (be <= 1e-13 * scale))[0]
+        k = int(bad[0]) + 1 if bad.size else j + 1  # T of size k: alphas[:k], betas[:k-1]
+        ev = eigvalsh_tridiagonal(al[:k], be[:k - 1]) if k > 1 else al[:1]
         theta = float(np.max(np.abs(ev))) if sym else float(ev[-1])
-        if b <= 1e-300 or (prev is not None and abs(theta - prev) <= tol * abs(theta)):
+        if bad.size or (prev is not None and abs(theta - prev) <= tol * abs(theta)):
             break
         prev = theta
-        betas.append(b)
-        Q[j + 1] = w / b
     return theta
 
 
@@ -137,16 +149,17 @@ class LinearOperator(DifferentiableMap):
         import scipy.sparse.linalg as spls
         return spls.svds(A=self.SciOp, k=k, which=which, return_singular_vectors=False, **kwargs)
 
-    def compute_lipschitz_cst(self, tol=1e-10, max_steps=300, **kwargs):
-        """Operator norm ``||K||_2`` by device Lanczos on ``K^T K`` (or ``|eig|`` if symmetric)."""
-        dtype = torch.float64
+    def compute_lipschitz_cst(self, tol=1e-9, max_steps=5000, **kwargs):
+        """Operator norm ``||K||_2`` (``pycsou/core/linop.py:279-321``: ARPACK ``svds`` / ``eigsh``
+        with k=1) by device Lanczos on ``K^T K`` (or ``|eig|`` if symmetric) in bounded memory
+        (a few vectors of the domain size, whatever the operator's size).  Other ARPACK keyword
+        arguments are accepted and ignored; ``tol`` is the relative change of the estimate
+        between checks at which the iteration stops."""
         if self.is_symmetric:
-            lam = _lanczos_sigma_max(lambda v: self._apply(v), self.shape[1], dtype, sym=True, tol=tol,
-                                     max_steps=max_steps)
+            lam = _lanczos_extreme(lambda v: self._apply(v), self.shape[1], sym=True, tol=tol, max_steps=max_steps)
             self.lipschitz_cst = float(abs(lam))
         else:
-            lam = _lanczos_sigma_max(lambda v: self._adj(self._apply(v)), self.shape[1], dtype, tol=tol,
-                                     max_steps=max_steps)
+            lam = _lanczos_extreme(lambda v: self._adj(self._apply(v)), self.shape[1], tol=tol, max_steps=max_steps)
             self.lipschitz_cst = float(np.sqrt(max(lam, 0.0)))
         self.diff_lipschitz_cst = self.lipschitz_cst
 

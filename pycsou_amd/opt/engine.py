@@ -6,7 +6,7 @@ kind='forward')``, ``H = lam * L21Norm(groups=tile(arange(N), 2))`` or ``lam * L
 ``G = None / NonNegativeOrthant / Segment``) and runs ``PrimalDualSplitting.iterate``
 (``pycsou/opt/proxalgs.py:343-394`` inside ``pycsou/core/solver.py:55-76``) as
 
-    per iteration:  [GRADBUF only: r = h*x - y ; g = h^T r]   (pcs_conv2d x2)
+    per iteration:  [GRADBUF only: r = h*x - y ; g = h^T r]   (pcs_conv2d_planned x2)
                     pcs_pds2d_step        x, z  ->  x', z', per-block norm partials
                     pcs_pds_reduce_finalize      -> relative improvements, iteration
                                                     counter, device stop flag
@@ -132,7 +132,9 @@ class PDS2DEngine:
             else:
                 fk = L.PCS_F_GRADBUF
                 self.conv = conv
-                conv._h.get(dtype), conv._hf.get(dtype)  # device PSF copies exist before capture
+                # device PSF copies / packed correlation plans exist before capture
+                conv._h.get(dtype), conv._hf.get(dtype)
+                self.plans = (conv.plan(dtype, False), conv.plan(dtype, True))
                 self.R = torch.empty(self.N, dtype=dtype, device=dev)
                 self.Gb = torch.empty(self.N, dtype=dtype, device=dev)
                 a.gbuf = self.Gb.data_ptr()
@@ -167,12 +169,7 @@ class PDS2DEngine:
     def _iteration(self, p, hist):
         a, lib, st = self.args, self.lib, L.stream()
         if self.fkind == L.PCS_F_GRADBUF:
-            c = self.conv
-            h, hf = c._h.get(self.dtype), c._hf.get(self.dtype)
-            L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.X[p]), L.ptr(self.R), c.dims[0], c.dims[1], L.ptr(h), c.kh,
-                                   c.kw, c.off[0], c.off[1], L.ptr(self.y), -1.0, st), 'pcs_conv2d')
-            L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.R), L.ptr(self.Gb), c.dims[0], c.dims[1], L.ptr(hf), c.kh,
-                                   c.kw, c.kh - 1 - c.off[0], c.kw - 1 - c.off[1], None, 0.0, st), 'pcs_conv2d')
+            self._grad_conv(p, st)
         a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
         a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
         a.hist = hist.data_ptr() if self.fused_finalize else None
@@ -180,6 +177,24 @@ class PDS2DEngine:
         if not self.fused_finalize:
             L.check(lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl), L.ptr(hist),
                                                 st), 'pcs_pds_reduce_finalize')
+
+    def _grad_conv(self, p, st):
+        """GRADBUF: r = h*x - y (residual fused into the forward pass), g = h^T r -- the
+        packed-plan correlation kernel (pcs_conv2d_planned) when the PSF fits its tiers."""
+        c, a, lib = self.conv, self.args, self.lib
+        fwd, adj = self.plans
+        n0, n1 = c.dims
+        if fwd is not None and adj is not None:
+            L.check(lib.pcs_conv2d_planned(a.dtype, L.ptr(self.X[p]), L.ptr(self.R), n0, n1, L.ptr(fwd[1]), fwd[0],
+                                           L.ptr(self.y), -1.0, st), 'pcs_conv2d_planned')
+            L.check(lib.pcs_conv2d_planned(a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(adj[1]), adj[0],
+                                           None, 0.0, st), 'pcs_conv2d_planned')
+            return
+        h, hf = c._h.get(self.dtype), c._hf.get(self.dtype)
+        L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.X[p]), L.ptr(self.R), n0, n1, L.ptr(h), c.kh, c.kw, c.off[0],
+                               c.off[1], L.ptr(self.y), -1.0, st), 'pcs_conv2d')
+        L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(hf), c.kh, c.kw,
+                               c.kh - 1 - c.off[0], c.kw - 1 - c.off[1], None, 0.0, st), 'pcs_conv2d')
 
     def _chunk(self, hist):
         for i in range(self.chunk):
@@ -208,6 +223,7 @@ class PDS2DEngine:
         """Device state for `total_iters` iterations that never stop early, captured in
         graphs of `chunk` (even) iterations."""
         self.chunk = chunk
+        self._fixed_p = 0
         hist_len = 2 * (total_iters + 1) + 2
         self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
         L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(total_iters), int(total_iters), -1.0, 1, hist_len,
@@ -224,6 +240,64 @@ class PDS2DEngine:
             self._chunk_native(self.hist)
         else:
             self.graph.replay()
+
+    def advance_fixed(self, n):
+        """Enqueue exactly n iterations of a prepare_fixed() loop, continuing from the buffer
+        parity the previous call left (odd counts allowed): native images as one
+        pcs_pds2d_run of n launches, graph images as whole captured chunks while the parity
+        allows plus eager single iterations."""
+        p = getattr(self, '_fixed_p', 0)
+        if self.native:
+            a = self.args
+            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            a.hist = self.hist.data_ptr()
+            L.check(self.lib.pcs_pds2d_run(ctypes.byref(a), int(n), L.stream()), 'pcs_pds2d_run')
+            self._fixed_p = p ^ (int(n) & 1)
+            return
+        while n >= self.chunk and p == 0:
+            self.graph.replay()
+            n -= self.chunk
+        for _ in range(n):
+            self._iteration(p, self.hist)
+            p ^= 1
+        self._fixed_p = p
+
+    def time_iteration_kernels(self, n):
+        """Mean duration (ms) of each kernel of an iteration over n eager iterations, HIP
+        events on the launching stream around every launch: {'step': ...} and, for a
+        non-separable PSF, {'conv_fwd': ..., 'conv_adj': ...}."""
+        a, lib = self.args, self.lib
+        st = torch.cuda.current_stream()
+        n = min(n, (self.hist.numel() - 2) // 2 - 1)
+        L.check(lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, int(self.hist.numel()), L.stream()),
+                'pcs_ctrl_init2')
+        names = ['conv_fwd', 'conv_adj', 'step'] if self.fkind == L.PCS_F_GRADBUF else ['step']
+        ev = {k: [] for k in names}
+
+        def timed(name, fn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            fn()
+            e1.record(st)
+            ev[name].append((e0, e1))
+        for i in range(n):
+            p = i % 2
+            if self.fkind == L.PCS_F_GRADBUF:
+                fwd, adj = self.plans
+                n0, n1 = self.conv.dims
+                timed('conv_fwd', lambda: L.check(lib.pcs_conv2d_planned(
+                    a.dtype, L.ptr(self.X[p]), L.ptr(self.R), n0, n1, L.ptr(fwd[1]), fwd[0], L.ptr(self.y), -1.0,
+                    L.stream()), 'pcs_conv2d_planned'))
+                timed('conv_adj', lambda: L.check(lib.pcs_conv2d_planned(
+                    a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(adj[1]), adj[0], None, 0.0, L.stream()),
+                    'pcs_conv2d_planned'))
+            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            a.hist = self.hist.data_ptr()
+            timed('step', lambda: L.check(lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step'))
+        torch.cuda.synchronize()
+        return {k: float(np.mean([s.elapsed_time(e) for s, e in v])) for k, v in ev.items()}
 
     def time_step_kernel(self, n, stream=None):
         """Average duration (ms) of the fused step kernel over `n` eager launches, measured

@@ -100,6 +100,9 @@ CASES = [
     ((300, 200), 0, 'l21', '', (1.0, 1.0)),            # denoising, partial last strip
     ((1030, 2048), 0, 'l1', 'segment', (2.0, 0.5)),    # denoising, C2 width, short last segment
     ((261, 132), -5, 'l21', 'nonneg', (1.0, 1.0)),     # non-separable 5x5 PSF (gradient buffer)
+    # non-separable PSFs through the packed-plan correlation kernel (corr2d.hip) + GRADBUF update
+    ((1000, 4096), -15, 'l21', 'nonneg', (1.0, 1.0)),  # C3 width, 15x15, several strip segments
+    ((517, 1000), -9, 'l1', '', (2.0, 0.5)),           # 9x9 (tier 9), ragged rows, non-unit steps
 ]
 
 

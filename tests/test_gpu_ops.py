@@ -382,6 +382,40 @@ def test_lipschitz_lanczos(A):
     assert abs(C.lipschitz_cst - np.linalg.norm(dense, 2)) < 1e-6
 
 
+@pytest.mark.parametrize('case', ['grad2d_4096', 'conv2d_4096', 'grad3d_512'])
+def test_lipschitz_scalable(A, case):
+    """compute_lipschitz_cst at the benchmark sizes (f1): bounded memory (a few vectors of the
+    domain, however large the operator) and the analytic constants bench.py used to hard-code,
+    to 1e-6 relative.  For the blur: nonnegative PSF of unit sum, so ||C|| <= 1 and the top
+    singular vector is smooth -- ||C|| = 1 up to the O((pi sigma / n)^2) boundary loss."""
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient
+    if case == 'grad3d_512':
+        n = 512
+        op = Gradient((n, n, n), kind='forward')
+        exact = np.sqrt(3 * 4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2)
+        N, tol = n ** 3, 1e-6
+    elif case == 'grad2d_4096':
+        n = 4096
+        op = Gradient((n, n), kind='forward')
+        exact = np.sqrt(2 * 4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2)
+        N, tol = n * n, 1e-6
+    else:
+        n = 4096
+        op = Convolve2D(n * n, OR.gaussian_psf(15, 2.0), (n, n))
+        exact, N, tol = 1.0, n * n, 1e-5
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    op.compute_lipschitz_cst()
+    torch.cuda.synchronize()
+    extra = torch.cuda.max_memory_allocated() - base
+    assert op.lipschitz_cst <= exact * (1 + 1e-9)
+    assert abs(op.lipschitz_cst - exact) <= tol * exact, (op.lipschitz_cst, exact)
+    d = op.shape[0] // N
+    assert extra <= (4 + d + 1) * N * 8, extra / (N * 8)
+
+
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 @pytest.mark.parametrize('ka,offa,kb,offb', [(15, 7, 15, 7), (15, 14, 15, 0), (6, 2, 9, 8)])
 @pytest.mark.parametrize('dims', [(4, 200, 264), (2, 1100, 128), (9, 17, 36), (3, 150, 131), (40, 64, 256)])
