@@ -264,9 +264,10 @@ class PDS2DEngine:
         self._fixed_p = p
 
     def time_iteration_kernels(self, n):
-        """Mean duration (ms) of each kernel of an iteration over n eager iterations, HIP
+        """Median duration (ms) of each kernel of an iteration over n eager iterations, HIP
         events on the launching stream around every launch: {'step': ...} and, for a
-        non-separable PSF, {'conv_fwd': ..., 'conv_adj': ...}."""
+        non-separable PSF, {'conv_fwd': ..., 'conv_adj': ...}.  (Median: a single launch
+        delayed by an unrelated host or driver event does not move it.)"""
         a, lib = self.args, self.lib
         st = torch.cuda.current_stream()
         n = min(n, (self.hist.numel() - 2) // 2 - 1)
@@ -297,7 +298,7 @@ class PDS2DEngine:
             a.hist = self.hist.data_ptr()
             timed('step', lambda: L.check(lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step'))
         torch.cuda.synchronize()
-        return {k: float(np.mean([s.elapsed_time(e) for s, e in v])) for k, v in ev.items()}
+        return {k: float(np.median([s.elapsed_time(e) for s, e in v])) for k, v in ev.items()}
 
     def time_step_kernel(self, n, stream=None):
         """Average duration (ms) of the fused step kernel over `n` eager launches, measured
