@@ -307,6 +307,8 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   return launch_status();
 }
 
+static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb);
+
 // persistent form: all n iterations in one launch; the grid must be co-resident
 template <int FK, int HK>
 static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hipStream_t st) {
@@ -320,9 +322,16 @@ static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hip
   // blocks of 256 threads per CU for a grid that must be co-resident
   nb = nb > 3 ? 3 : nb;  // and 3 per CU is the fastest grid of the per-launch kernel too
   if (tiles_x < 2 || nb < 1) return PCS_EUNSUPPORTED;
-  MarchPlan p;  // one wave of this kernel's resident workgroups
-  plan_bands(full_bands(a), PtGeom::TS, tiles_x, cus * nb, 4, &p);
-  if (p.ntasks < 1 || (int64_t)p.ntasks > (int64_t)cus * nb) return PCS_EUNSUPPORTED;
+  // one wave of this kernel's resident workgroups, and never more tasks than the per-launch
+  // plan that sized the caller's partials / ws buffers (pcs_pds2d_nblocks, pt_slots())
+  const int slots = cus * nb < pt_slots() ? cus * nb : pt_slots();
+  MarchPlan p;
+  plan_bands(full_bands(a), PtGeom::TS, tiles_x, slots, 4, &p);
+  if (p.ntasks < 1 || (int64_t)p.ntasks > (int64_t)cus * nb || (int64_t)p.ntasks > bands_nblocks(a, full_bands(a)))
+    return PCS_EUNSUPPORTED;
+  // fresh barrier state for every launch: a timed-out barrier of an earlier launch (sticky
+  // flag, stranded arrival count) cannot leak into this one
+  if (hipMemsetAsync(bar, 0, (size_t)pcs_grid_bar_bytes(), st) != hipSuccess) return PCS_ELAUNCH;
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);

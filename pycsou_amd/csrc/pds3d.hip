@@ -346,14 +346,19 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
   const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
   const int64_t bands = (L0 > 0) + (L1 > 0);
-  // as few plane segments as give one workgroup per CU (256 CUs): long marches amortise the
+  // as few plane segments as give one workgroup per CU (the device's CU count): long marches amortise the
   // two-plane ring prologue; C4 512^3: 0.92 ms at 256 tasks against 0.95 at 1024 (paired runs)
   // (profiles/r1_3d_grid_sweep.txt); never segments shorter than 8 planes
-  static int64_t target = 0;
-  if (target == 0) {
+  static const int64_t target = [] {
     const char* e = getenv("PCS_3D_TARGET");  // diagnostics: grid-size sweep
-    target = e && atoll(e) > 0 ? atoll(e) : 256;
-  }
+    if (e && atoll(e) > 0) return (int64_t)atoll(e);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    (void)hipGetLastError();
+    return (int64_t)cus;  // one 512-thread workgroup per CU
+  }();
   int64_t nseg = (target + per_plane - 1) / per_plane;
   const int64_t max_seg = (L + 7) / 8;
   nseg = nseg > max_seg ? max_seg : nseg;

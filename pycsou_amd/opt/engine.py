@@ -355,7 +355,7 @@ class PDS2DEngine:
                 pending.append(ev)
                 if len(pending) >= 2:
                     pending.pop(0).synchronize()
-                    if int(self.ctrl_host[1]) != 0:
+                    if int(self.ctrl_host[1]) != 0 or (self.persistent and self.barrier_timed_out()):
                         break
         else:
             for k in range(n_chunks):
@@ -363,6 +363,11 @@ class PDS2DEngine:
                 if int(self.ctrl.view(torch.int32)[1].item()) != 0:
                     break
         torch.cuda.synchronize()
+        if self.persistent and self.barrier_timed_out():
+            # a persistent chunk's grid barrier gave up: x / z hold a mix of iterations and the
+            # loop control is inconsistent -- never return that as a result
+            raise RuntimeError('pcs_pds2d_run_persistent: grid barrier timed out (workgroups not co-resident); '
+                               'rerun without PCS_PERSISTENT=1')
         c = self.ctrl.view(torch.int32)[:2].cpu().numpy()
         n = int(c[0])
         h = hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
