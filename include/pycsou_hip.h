@@ -168,6 +168,13 @@ int pcs_axpby(int dtype, const void* x, const void* y, void* out, int64_t n, dou
 /* out = (x - a*y) - b*w  (the PDS primal argument, proxalgs.py:348). */
 int pcs_sub2(int dtype, const void* x, const void* y, const void* w, void* out, int64_t n, double a, double b,
              hipStream_t stream);
+/* out = d * x elementwise (DiagonalOperator with a vector diagonal, pycsou/linop/base.py:551-579). */
+int pcs_mul(int dtype, const void* x, const void* d, void* out, int64_t n, hipStream_t stream);
+/* The two sums of one relative improvement ||old - new|| / ||old|| (proxalgs.py:370-383) in one
+ * pass, fixed order: out_dev[0] = sum (old - new)^2, out_dev[1] = sum old^2 (the layout
+ * pcs_pds_finalize reads).  ws >= pcs_reduce_ws_bytes(). */
+int pcs_rel_sums(int dtype, const void* old, const void* nw, int64_t n, double* out_dev, void* ws,
+                 hipStream_t stream);
 /* Deterministic fp64 reductions into out_dev[0]: kind 0 = sum x^2, 1 = sum |x|,
  * 2 = sum (x-y)^2, 3 = sum x*y.  ws >= pcs_reduce_ws_bytes(). */
 int64_t pcs_reduce_ws_bytes(void);

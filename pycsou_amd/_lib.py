@@ -97,6 +97,8 @@ _SIGS = {
     'pcs_proj_nonneg': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
     'pcs_proj_segment': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
     'pcs_axpby': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
+    'pcs_mul': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _vp]),
+    'pcs_rel_sums': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp, _vp, _vp]),
     'pcs_sub2': (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _vp]),
     'pcs_reduce_ws_bytes': (_c_i64, []),
     'pcs_reduce': (_c_int, [_c_int, _c_int, _vp, _vp, _c_i64, _vp, _vp, _vp]),

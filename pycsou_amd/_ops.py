@@ -89,6 +89,22 @@ def add(x, y):
     return axpby(x, y, 1.0, 1.0)
 
 
+def mul(x, d):
+    """d * x elementwise (pcs_mul)."""
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    L.check(lib.pcs_mul(L.dtcode(x), L.ptr(x), L.ptr(d), L.ptr(out), x.numel(), L.stream()), 'pcs_mul')
+    return out
+
+
+def rel_sums(old, new, out):
+    """out[0], out[1] = sum (old - new)^2, sum old^2 (fp64, fixed order) into a device slice."""
+    lib = L.gpu()
+    L.check(lib.pcs_rel_sums(L.dtcode(old), L.ptr(old), L.ptr(new), old.numel(), L.ptr(out), L.ptr(_ws(old)),
+                             L.stream()), 'pcs_rel_sums')
+    return out
+
+
 def sub2(x, y, w, a, b):
     """(x - a*y) - b*w  (proxalgs.py:348)."""
     lib = L.gpu()

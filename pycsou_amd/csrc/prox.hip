@@ -136,7 +136,45 @@ __global__ void k_sub2(const T* __restrict__ x, const T* __restrict__ y, const T
   PCS_GRID_LOOP(p, n) out[p] = (x[p] - a * y[p]) - b * w[p];
 }
 
+template <typename T>
+__global__ void k_mul(const T* __restrict__ x, const T* __restrict__ d, T* __restrict__ out, int64_t n) {
+  PCS_GRID_LOOP(p, n) out[p] = d[p] * x[p];
+}
+
 constexpr int kRedBlocks = 1024;
+
+// both sums of one relative improvement in one pass: part[b] = (sum (a-b)^2, sum a^2) of block b
+template <typename T>
+__global__ __launch_bounds__(256) void k_relsums_stage1(const T* __restrict__ old, const T* __restrict__ nw,
+                                                        int64_t n, double* __restrict__ part) {
+  __shared__ double sm[8];
+  double v[2] = {0.0, 0.0};
+  PCS_GRID_LOOP(p, n) {
+    const double a = (double)old[p], dd = a - (double)nw[p];
+    v[0] += dd * dd;
+    v[1] += a * a;
+  }
+  block_sum<2>(v, sm);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = v[0];
+    part[2 * blockIdx.x + 1] = v[1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_relsums_stage2(const double* __restrict__ part, int np,
+                                                        double* __restrict__ out) {
+  __shared__ double sm[8];
+  double v[2] = {0.0, 0.0};
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    v[0] += part[2 * i];
+    v[1] += part[2 * i + 1];
+  }
+  block_sum<2>(v, sm);
+  if (threadIdx.x == 0) {
+    out[0] = v[0];
+    out[1] = v[1];
+  }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_reduce_stage1(int kind, const T* __restrict__ x, const T* __restrict__ y,
@@ -311,6 +349,20 @@ int pcs_proj_segment(int dt, const void* x, void* out, int64_t n, double a, doub
 int pcs_axpby(int dt, const void* x, const void* y, void* out, int64_t n, double a, double b, hipStream_t st) {
   if (!x || !out || n < 0) return PCS_EINVAL;
   PCS_DISPATCH(dt, k_axpby<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (const T*)y, (T*)out, n, (T)a, (T)b));
+  return launch_status();
+}
+
+int pcs_mul(int dt, const void* x, const void* d, void* out, int64_t n, hipStream_t st) {
+  if (!x || !d || !out || n < 0) return PCS_EINVAL;
+  PCS_DISPATCH(dt, k_mul<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, (const T*)d, (T*)out, n));
+  return launch_status();
+}
+
+int pcs_rel_sums(int dt, const void* old, const void* nw, int64_t n, double* out_dev, void* ws, hipStream_t st) {
+  if (!old || !nw || !out_dev || !ws || n < 0) return PCS_EINVAL;
+  const unsigned g = grid_for(n, 256, kRedBlocks / 2);
+  PCS_DISPATCH(dt, k_relsums_stage1<T><<<g, 256, 0, st>>>((const T*)old, (const T*)nw, n, (double*)ws));
+  k_relsums_stage2<<<1, 256, 0, st>>>((const double*)ws, (int)g, out_dev);
   return launch_status();
 }
 

@@ -79,7 +79,7 @@ class DiagonalOperator(LinearOperator):
             return float(self.diag[0]) * t
         if self.diag.size == 1:
             return O.scale(t, float(self.diag[0]))
-        return t * self._d(t.dtype)
+        return O.mul(t, self._d(t.dtype))
 
     def _adj(self, t):
         return self._apply(t)

@@ -61,11 +61,66 @@ def _wants_torch(*objs):
 
 
 def _rel_improvement(old, new):
-    """||old - new|| / ||old|| (inf if ||old|| == 0), proxalgs.py:370-383."""
-    n_old = float(O.reduce_dev(0, old).item())
-    if n_old == 0:
+    """||old - new|| / ||old|| (inf if ||old|| == 0), proxalgs.py:370-383: both sums in one
+    device pass, one read-back (API-level update_diagnostics; the solver loops use _DeviceLoop)."""
+    d2, n2 = O.rel_sums(old, new, torch.empty(2, dtype=torch.float64, device=old.device)).tolist()
+    if n2 == 0:
         return np.inf
-    return float(np.sqrt(O.reduce_dev(2, old, new).item()) / np.sqrt(n_old))
+    return float(np.sqrt(d2) / np.sqrt(n2))
+
+
+class _DeviceLoop:
+    """Loop control of the per-operator (generic) path on the device: after each iteration the
+    relative-improvement sums are reduced on the GPU (pcs_rel_sums) and pcs_pds_finalize
+    records the diagnostics row and the reference loop condition (solver.py:65-66,
+    proxalgs.py:366-394) in a device control block -- the same one the fused engine uses.
+    The host learns the stop decision from an asynchronous copy of that block, up to ``lag``
+    iterations behind (no blocking .item() per iteration); iterations issued past the stop
+    are discarded by the caller, which keeps the last ``lag + 2`` states."""
+
+    def __init__(self, max_iter, min_iter, thr, has_dual, device, lag=3):
+        from .. import _lib as L
+        self.L, self.lib = L, L.gpu()
+        self.total = max(min_iter, max_iter) + 1
+        self.hist = torch.full((2 * self.total + 2,), float('nan'), dtype=torch.float64, device=device)
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=device)
+        self.sums = torch.zeros(4, dtype=torch.float64, device=device)
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(thr), int(has_dual),
+                                        int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
+        self.has_dual, self.lag = has_dual, lag
+        self.pending = []  # (pinned host copy of (it, stopped), event)
+        self.final = None
+
+    def record(self, x_old, x, z_old=None, z=None):
+        """Enqueue this iteration's sums + finalize and an async read-back of the control."""
+        L = self.L
+        O.rel_sums(x_old, x, self.sums[0:2])
+        if self.has_dual:
+            O.rel_sums(z_old, z, self.sums[2:4])
+        L.check(self.lib.pcs_pds_finalize(L.ptr(self.sums), L.ptr(self.ctrl), L.ptr(self.hist), L.stream()),
+                'pcs_pds_finalize')
+        host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        host.copy_(self.ctrl.view(torch.int32)[:2], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((host, ev))
+
+    def poll(self, drain=False):
+        """Resolve finished read-backs in order; returns the iteration count once the device
+        stopped (None while it runs).  Blocks only to keep at most ``lag`` in flight."""
+        while self.pending and self.final is None:
+            host, ev = self.pending[0]
+            if not (drain or len(self.pending) > self.lag or ev.query()):
+                break
+            ev.synchronize()
+            self.pending.pop(0)
+            if int(host[1]) != 0:
+                self.final = int(host[0])
+        return self.final
+
+    def rows(self, n):
+        h = self.hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
+        return h
 
 
 class PrimalDualSplitting(GenericIterativeAlgorithm):
@@ -226,20 +281,40 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
 
     # ---------------------------------------------------------------- generic device path
     def _iterate_generic(self):
+        """The reference loop (solver.py:55-76) operator by operator on the device, with the
+        stopping rule evaluated on the device (``_DeviceLoop``): up to ``lag`` iterations are
+        issued ahead of the stop decision and discarded if the reference would have stopped."""
         dtype = self._compute_dtype()
-        self._state = {'primal_variable': O.to_dev(self.x0, dtype),
-                       'dual_variable': None if self.z0 is None else O.to_dev(self.z0, dtype)}
-        self._old = dict(self._state)
-        self._rows = []
-        self.init_iterand_dev = dict(self._state)
-        while ((self.iter <= self.max_iter) and (self.stopping_metric() > self.accuracy_threshold)) or (
-                self.iter <= self.min_iter):
-            self._state = self._update_dev(self._state)
-            self.update_diagnostics()
-            if self.verbose is not None and self.iter % self.verbose == 0:
+        state = {'primal_variable': O.to_dev(self.x0, dtype),
+                 'dual_variable': None if self.z0 is None else O.to_dev(self.z0, dtype)}
+        self.init_iterand_dev = dict(state)
+        loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, bool(self._H),
+                           state['primal_variable'].device)
+        states = {-1: state}
+        i, n = 0, None
+        while n is None:
+            if i >= loop.total:
+                n = loop.poll(drain=True)
+                break
+            new = self._update_dev(states[i - 1])
+            loop.record(states[i - 1]['primal_variable'], new['primal_variable'],
+                        states[i - 1]['dual_variable'], new['dual_variable'])
+            states[i] = new
+            states.pop(i - loop.lag - 3, None)
+            i += 1
+            n = loop.poll()
+        self.iter = n
+        h = loop.rows(n)
+        self._rows = [[k, h[k, 0], h[k, 1]] if self._H else [k, h[k, 0]] for k in range(n)]
+        if self.verbose is not None:
+            # the reference prints row ``iter`` every ``verbose`` iterations inside its loop
+            # (solver.py:69-71); here the rows come from the device history after the loop
+            rows = self._rows
+            for row in rows[::self.verbose]:
+                self._rows = [row]
                 self.print_diagnostics()
-            self._old = self._state
-            self.iter += 1
+            self._rows = rows
+        self._state = states[n - 1]
         self.converged = True
         cols = ['Iter', 'Relative Improvement (primal variable)']
         if self._H:
@@ -351,19 +426,42 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         return t if self._torch_out else t.detach().cpu().numpy()
 
     def iterate(self):
+        """The reference loop (solver.py:55-76) with the stopping rule evaluated on the device
+        (``_DeviceLoop``; the fused step writes its two norms straight into the loop's sums)."""
         dtype = self._compute_dtype()
         x0 = O.to_dev(self.x0, dtype)
-        self._state = (x0, torch.zeros_like(x0), 1)
-        self._old = x0
-        self._rows = []
-        while ((self.iter <= self.max_iter) and (self.stopping_metric() > self.accuracy_threshold)) or (
-                self.iter <= self.min_iter):
-            self._state = self._update_dev(self._state)
-            self.update_diagnostics()
-            if self.verbose is not None and self.iter % self.verbose == 0:
+        loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, False, x0.device)
+        states = {-1: (x0, torch.zeros_like(x0), 1)}
+        i, n = 0, None
+        while n is None:
+            if i >= loop.total:
+                n = loop.poll(drain=True)
+                break
+            self.iter = i  # the 'CD' momentum reads the iteration index (proxalgs.py:596-598)
+            new = self._update_dev(states[i - 1], sums_out=loop.sums[0:2])
+            if self._sums is None:
+                O.rel_sums(states[i - 1][0], new[0], loop.sums[0:2])
+            loop.L.check(loop.lib.pcs_pds_finalize(loop.L.ptr(loop.sums), loop.L.ptr(loop.ctrl),
+                                                   loop.L.ptr(loop.hist), loop.L.stream()), 'pcs_pds_finalize')
+            host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+            host.copy_(loop.ctrl.view(torch.int32)[:2], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            loop.pending.append((host, ev))
+            states[i] = new
+            states.pop(i - loop.lag - 3, None)
+            i += 1
+            n = loop.poll()
+        self.iter = n
+        h = loop.rows(n)
+        self._rows = [[k, h[k, 0]] for k in range(n)]
+        if self.verbose is not None:
+            rows = self._rows
+            for row in rows[::self.verbose]:
+                self._rows = [row]
                 self.print_diagnostics()
-            self._old = self._state[0]
-            self.iter += 1
+            self._rows = rows
+        self._state = states[n - 1]
         self.converged = True
         self.diagnostics = _frame(['Iter', 'Relative Improvement'], self._rows)
         x, aux, t = self._state
@@ -398,7 +496,7 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
             t = t_old = 1
         return t, (t_old - 1) / t
 
-    def _update_dev(self, st):
+    def _update_dev(self, st, sums_out=None):
         """``proxalgs.py:586-601``: G.prox, the momentum step and the diagnostics' two norms in
         one kernel (pcs_apgd_step) when G is null / lam*L1 / an orthant or segment indicator."""
         x, x_old, t_old = st
@@ -406,7 +504,8 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         gk = self._g_kind()
         if gk is not None:
             kind, lam, seg = gk
-            xn, x_temp, self._sums = O.apgd_step(x, self.F._grad(x), x_old, self.tau, a, kind, lam, seg)
+            xn, x_temp, self._sums = O.apgd_step(x, self.F._grad(x), x_old, self.tau, a, kind, lam, seg,
+                                                 sums=sums_out)
             return (xn, x_temp, t)
         self._sums = None
         x_temp = self.G._prox(O.axpby(x, self.F._grad(x), 1.0, -self.tau), self.tau)

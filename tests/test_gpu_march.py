@@ -133,3 +133,36 @@ def test_march_is_the_kernel_in_use():
     a.step0 = a.step1 = 1.0
     nb = L.load().pcs_pds2d_nblocks(ctypes.byref(a))
     assert nb == 4 * 19
+
+
+def test_c2_full_size_fused_vs_generic():
+    """C2 exactly (BASELINE configs[1]): 2048^2 fp32 isotropic-TV denoising, 0.1 * L21Norm,
+    Gradient(kind='forward'), 12 iterations -- the fused row-marching engine against the
+    per-operator generic path (separate Gradient / L21 / axpby kernels, device loop control):
+    same iteration count, x and z to 1e-5 relative (fp32 rounding of two different op
+    orders), diagnostics to 1e-3 relative."""
+    import torch
+
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    n = 2048
+    N = n * n
+    y = torch.as_tensor((OR.phantom((n, n), seed=3) + 0.1 * np.random.default_rng(3).standard_normal((n, n)))
+                        .astype(np.float32).ravel()).cuda()
+    out = {}
+    for mode in ('fused', 'generic'):
+        K = Gradient((n, n), kind='forward')
+        K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(8 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+        pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y), H=0.1 * L21Norm(dim=2 * N,
+                  groups=np.tile(np.arange(N), 2)), K=K, x0=torch.zeros(N, device='cuda'),
+                  z0=torch.zeros(2 * N, device='cuda'), max_iter=NITER - 1, min_iter=NITER - 1,
+                  accuracy_threshold=0.0, verbose=None, engine=mode)
+        est, _, diag = pds.iterate()
+        assert (pds._engine is not None) == (mode == 'fused') and pds.iter == NITER
+        out[mode] = (est['primal_variable'].cpu().numpy(), est['dual_variable'].cpu().numpy(), diag)
+    (xf, zf, df), (xg, zg, dg) = out['fused'], out['generic']
+    assert rel(xf, xg) < 1e-5 and rel(zf, zg) < 1e-5
+    for col in ('Relative Improvement (primal variable)', 'Relative Improvement (dual variable)'):
+        np.testing.assert_allclose(df[col].to_numpy(float)[1:], dg[col].to_numpy(float)[1:], rtol=1e-3)
