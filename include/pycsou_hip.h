@@ -112,6 +112,16 @@ int pcs_conv2d_sep_planes(int dtype, const void* in, void* out, int64_t nplanes,
                           const void* ha, int ka, int offa, const void* hb, int kb, int offb, int vfirst,
                           hipStream_t stream);
 
+/* In-plane normal operator of a separable blur, every plane in one pass (pycsou/linop/conv.py:20-164
+ * along axes 1 and 2; the in-plane half of grad F = C^T (C x - y), core/map.py:609-610):
+ *   out = C_a^T C_b^T C_b C_a in   (C_a along axis 1: ha, ka, offa; C_b along axis 2: hb, kb, offb;
+ *                                   zero boundary between the passes, as the four pcs_conv1d calls)
+ * in != out, 16-B aligned, ka, kb <= 15.  PCS_EUNSUPPORTED when n2 % 4 != 0 or the horizontal
+ * offset cannot be fitted to the strip layout (15-tap filter with offb % 4 == 1); nplanes == 0
+ * only validates. */
+int pcs_conv2d_sep_ata_planes(int dtype, const void* in, void* out, int64_t nplanes, int64_t n1, int64_t n2,
+                              const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t stream);
+
 /* The axis-0 stage of grad F = C^T (C x - y) for a 3-D Convolve1D chain, in one pass
  * (pycsou/linop/conv.py:20-164 along axis 0, residual of core/map.py:609-610): on sub-volumes
  * of nsub planes of `plane` elements,

@@ -85,6 +85,8 @@ _SIGS = {
     'pcs_conv1d': (_c_int, [_c_int, _vp, _vp, _c_int, _pi64, _c_int, _vp, _c_int, _c_int, _vp]),
     'pcs_conv2d_sep_planes': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_int, _c_int, _vp, _c_int,
                                         _c_int, _c_int, _vp]),
+    'pcs_conv2d_sep_ata_planes': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_int, _c_int, _vp,
+                                            _c_int, _c_int, _vp]),
     'pcs_conv0_residual_adjoint': (_c_int, [_c_int, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_int, _c_int, _c_i64,
                                              _c_i64, _c_i64, _c_i64, _vp]),
     'pcs_prox_l1': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp]),

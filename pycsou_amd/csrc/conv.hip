@@ -11,6 +11,7 @@
 // accumulates a column of TH/4 outputs with a rolling register window over the
 // apron rows so every LDS value read feeds up to TH/4 FMAs.
 #include "common.hpp"
+#include "vecio.hpp"
 
 namespace pcs {
 
@@ -129,22 +130,6 @@ static int conv2d(const void* x, void* out, int64_t n0, int64_t n1, const void* 
 
 // ---- fast paths for taps k <= 15 (zero-padded to 15: out[j] = sum_{t<15} h'[t] x[j + off - t])
 constexpr int kC1K = 15;
-
-template <typename T>
-struct V16 {  // 16 bytes of T
-  static constexpr int N = 16 / sizeof(T);
-  T v[N];
-};
-template <typename T>
-__device__ __forceinline__ V16<T> ldv(const T* p) {
-  V16<T> r;
-  *reinterpret_cast<uint4*>(r.v) = *reinterpret_cast<const uint4*>(p);
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ void stv(T* p, const V16<T>& r) {
-  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(r.v);
-}
 
 // Strided axis (stride sa >= 16 B, 16-B aligned rows): a thread owns 16 B of consecutive inner
 // elements and RUN consecutive outputs along the axis; every input row it streams feeds up to
@@ -372,50 +357,6 @@ static int conv0_rta(const void* t, const void* y, void* s, int64_t nsub, int64_
 // 64 + 32 columns, zeros outside the plane) is staged in LDS once, the first pass writes an LDS
 // intermediate, the second pass writes the output: 2 sub-volume passes instead of 4.  Each
 // output is the same t-ascending sum as pcs_conv1d's.
-template <typename T>
-struct Q4 {
-  T v[4];
-};
-template <typename T>
-__device__ __forceinline__ Q4<T> ldq(const T* p) {  // 4 elements, 16-B aligned
-  Q4<T> r;
-  constexpr int VN = V16<T>::N;
-#pragma unroll
-  for (int h = 0; h < 4 / VN; ++h) {
-    const V16<T> v = ldv(p + h * VN);
-#pragma unroll
-    for (int e = 0; e < VN; ++e) r.v[h * VN + e] = v.v[e];
-  }
-  return r;
-}
-// LDS read of 4 elements that stays whole 16-B ds_read_b128 (volatile, LDS address space):
-// otherwise hipcc narrows a read whose edge elements are unused into ds_read2_b32 pairs
-// (32-bank, 2-4 way conflicts)
-template <typename T>
-__device__ __forceinline__ Q4<T> ldsq(const T* p) {
-  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) const volatile u4* lds_u4;
-  Q4<T> r;
-  constexpr int VN = V16<T>::N;
-#pragma unroll
-  for (int h = 0; h < 4 / VN; ++h) {
-    const u4 v = ((lds_u4)(p))[h];
-    __builtin_memcpy(r.v + h * VN, &v, 16);
-  }
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ void stq(T* p, const Q4<T>& r) {
-  constexpr int VN = V16<T>::N;
-#pragma unroll
-  for (int h = 0; h < 4 / VN; ++h) {
-    V16<T> v;
-#pragma unroll
-    for (int e = 0; e < VN; ++e) v.v[e] = r.v[h * VN + e];
-    stv(p + h * VN, v);
-  }
-}
-
 constexpr int64_t kSep2DBlocks = 1024;
 
 // vertical pass over an LDS buffer: acc[r] = sum_t ha[t] rows[i + r + KT - 1 - t] at column c;

@@ -1,0 +1,365 @@
+// In-plane normal operator of a separable 3-D blur, every plane in one pass:
+//
+//   out = C_a^T C_b^T C_b C_a in        (C_a: Convolve1D along axis 1, C_b: along axis 2)
+//
+// i.e. the in-plane half of grad F = C^T (C x - y) for the reference's 3-D deconvolution
+// (pycsou/linop/conv.py:20-164 per axis; residual and adjoint of core/map.py:609-610).  The
+// axis-0 pass commutes with the in-plane ones, so the 3-D engine computes
+//   g = C_0^T (C_0 (C_12^T C_12 x) - C_12^T y)
+// with C_12^T y formed once at setup: two sub-volume passes per iteration (this kernel, then
+// pcs_conv0_residual_adjoint) instead of three, 5 words per voxel of traffic instead of 7.
+//
+// Four 15-tap passes per plane, marched down a 128-column strip 32 rows per step:
+//   P1  horizontal conv  (staging  -> ring A, 144 columns: the strip + the reach of P4)
+//   P2  vertical conv    (ring A   -> ring B, rows outside the image forced to 0)
+//   P3  vertical corr    (ring B   -> P3 rows, aliasing the staging buffer)
+//   P4  horizontal corr  (P3 rows  -> HBM, the strip's 128 columns)
+// Rings hold 48 rows (the 14-row reach of the vertical passes above a step), so no row is
+// filtered twice; a strip's horizontal halo (16 columns) is recomputed by P1-P3 (1.125x).
+// Zero boundary: input outside the plane reads 0, and P1 / P2 outputs outside the plane
+// are 0 (the truncation between C and C^T).  Taps are zero-padded to 15 (out[j] =
+// sum_t h'[t] in[j + o - t], h'[t] = h[t - pad], o = off + pad); the adjoint passes use
+// h'[14 - t] with offset 14 - o.  Persistent grid, tasks (plane, row segment, strip) with the
+// strip fastest and an XCD-aware task map, as k_sep2d_march.
+#include "vecio.hpp"
+
+namespace pcs {
+
+struct AtaG {
+  static constexpr int KT = 15, TX = 128, GX = TX / 4, GE = GX + 4, WE = 4 * GE, GI = GE + 4, WI = 4 * GI;
+  static constexpr int RS = 32, RING = 48, NT = 576;
+  static constexpr int NIN = RS * GI, NL = (NIN + NT - 1) / NT;  // staging loads per thread
+  static constexpr int NP1 = RS * GE, NP4 = RS * GX;             // P1 / P4 items
+  static_assert((RS / 2) * GE == NT, "at most one vertical item (2 or 4 rows x 4 columns) per thread");
+  static_assert(RING >= RS + KT - 1, "ring holds the 14 rows above a step");
+};
+
+
+#ifndef PCS_ATA_RB
+#define PCS_ATA_RB 2
+#endif
+#ifndef PCS_ATA_HREG
+#define PCS_ATA_HREG 0
+#endif
+
+// one vertical 15-tap pass over a ring of rows: acc[r] = sum_t h(t) ring[(base + r0 + r - t) mod RING]
+// at 4-column group q, h(t) = hv[t] (conv) or hv[14 - t] (FLIP: correlation); each of the RB + 14
+// ring rows is read once
+template <typename T, int RB, bool FLIP>
+__device__ __forceinline__ void vert_pass(const T* ring, int base, int r0, int q, const T* hv, Q4<T> (&acc)[RB]) {
+  using A = AtaG;
+  constexpr int KT = A::KT, RING = A::RING, WE = A::WE;
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
+#pragma unroll 2
+  for (int j = 0; j < KT - 1 + RB; ++j) {  // ring rows base + r0 - 14 + j
+    int slot = base + r0 - (KT - 1) + j;
+    slot = slot < 0 ? slot + RING : (slot >= RING ? slot - RING : slot);
+    const Q4<T> v = ldsq(ring + slot * WE + 4 * q);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int t = r + KT - 1 - j;
+      if (t >= 0 && t < KT) {
+        const T h = FLIP ? hv[KT - 1 - t] : hv[t];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[r].v[m] += h * v.v[m];
+      }
+    }
+  }
+}
+
+template <typename T, int SH4>
+__global__ __launch_bounds__(AtaG::NT) void k_sep2d_ata(const T* __restrict__ in, T* __restrict__ out, int n1, int n2,
+                                                         int nstrips, int nseg, int seg_len, int64_t ntasks,
+                                                         const T* __restrict__ ha_, int ka, const T* __restrict__ hb_,
+                                                         int kb, int o1, int padb, int o2) {
+  using A = AtaG;
+  constexpr int KT = A::KT, TX = A::TX, GE = A::GE, WE = A::WE, WI = A::WI, GI = A::GI, RS = A::RS, RING = A::RING,
+                NT = A::NT, NL = A::NL;
+  constexpr int SH1 = 2 - SH4;  // P1's window shift: the staged input starts 16 columns left of the strip
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* stg = reinterpret_cast<T*>(smem_raw);  // RS x WI input rows; P3 rows (RS x WE) after P1
+  T* ringA = stg + RS * WI;                 // RING x WE
+  T* ringB = ringA + RING * WE;             // RING x WE
+  // taps in LDS (broadcast reads, re-read per phase): 30 fp64 taps in registers spill at the
+  // 168-VGPR budget of 9 waves per workgroup.  hv: [0, 15), hh: [16, 31)
+  T* hv = ringB + RING * WE;
+  T* hh = hv + 16;
+  if (threadIdx.x < 16) {
+    const int t = threadIdx.x;
+    hv[t] = t < ka ? ha_[t] : T(0);
+    hh[t] = (t >= padb && t - padb < kb) ? hb_[t - padb] : T(0);
+  }
+#if PCS_ATA_HREG
+  T hreg[KT];  // horizontal taps in registers (P1 / P4 read each once per 4 outputs)
+#pragma unroll
+  for (int t = 0; t < KT; ++t) hreg[t] = (t >= padb && t - padb < kb) ? hb_[t - padb] : T(0);
+#define PCS_HH(t) hreg[t]
+#else
+#define PCS_HH(t) hh[t]
+#endif
+  int64_t t0, t_end, t_stride;
+  {  // XCD x owns a contiguous share of the task list; its blocks take consecutive tasks
+    const int64_t b = blockIdx.x, nb = gridDim.x, xcd = b % 8, k = b / 8, q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (xcd < r ? 1 : 0);
+    const int64_t before = xcd * q + (xcd < r ? xcd : r);
+    const int64_t lo = ntasks * before / nb, hi = ntasks * (before + nbx) / nb;
+    t0 = lo + k;
+    t_end = hi;
+    t_stride = nbx;
+  }
+  if (t0 >= t_end) return;
+  const int tid = threadIdx.x;
+  struct Cur {
+    int64_t t, plane;
+    int strip, a, b, s, ns;
+  };
+  auto task_at = [&](int64_t t) {
+    Cur c;
+    c.t = t;
+    const int64_t per_plane = (int64_t)nseg * nstrips;
+    c.plane = t / per_plane;
+    const int rem = (int)(t - c.plane * per_plane), seg = rem / nstrips;
+    c.strip = rem - seg * nstrips;
+    c.a = seg * seg_len;
+    c.b = min(n1, c.a + seg_len);
+    c.s = 0;
+    c.ns = (c.b - c.a + 2 * (KT - 1) + RS - 1) / RS;
+    return c;
+  };
+  Q4<T> q[NL];
+  // staging rows of step c: input rows L1 + s RS + r (L1 = a - 14), columns c0 - 16 + 4 g
+  auto prefetch = [&](const Cur& c) {
+    const T* src = in + c.plane * (int64_t)n1 * n2;
+    const int kmax = c.b - c.a + 2 * (KT - 1) - 1;  // last staged row any output of [a, b) needs
+    const int gc0 = c.strip * TX - 16;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = min(l * NT + tid, A::NIN - 1);
+      const int rr = e / GI, g = e - rr * GI;
+      const int k = c.s * RS + rr, gi = c.a - (KT - 1) + k, gc = gc0 + 4 * g;
+      const bool ok = gi >= 0 && gi < n1 && k <= kmax && gc >= 0 && gc + 4 <= n2;
+      const Q4<T> v = ldq(src + (ok ? (int64_t)gi * n2 + gc : 0));
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
+    }
+  };
+  Cur cur = task_at(t0);
+  prefetch(cur);
+  constexpr int RB = PCS_ATA_RB, NV = (RS / RB) * GE;  // vertical items: RB rows x one 4-column group
+  const int vrb = tid / GE, vq = tid - (tid / GE) * GE;  // vertical item: rows RB vrb .. + RB - 1; group vq
+  for (;;) {
+    lds_barrier();  // the previous step's P4 is done with the P3 rows (staging)
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = l * NT + tid;
+      if (e < A::NIN) stq(stg + 4 * e, q[l]);
+    }
+    Cur nxt = cur;
+    bool more = true;
+    if (cur.s + 1 < cur.ns) {
+      nxt.s = cur.s + 1;
+    } else {
+      more = cur.t + t_stride < t_end;
+      if (more) nxt = task_at(cur.t + t_stride);
+    }
+    if (more) prefetch(nxt);
+    const int c0 = cur.strip * TX;
+    const int e0 = c0 - o2 - SH4;  // first P1 column (E0, a multiple of 4); E0 + WE covers P4's reach
+    const int base = (cur.s * RS) % RING;  // ring slot of the step's first row
+    lds_barrier();
+    // ---- P1: horizontal conv of the RS staged rows, columns [E0, E0 + WE) -> ring A
+#pragma unroll 1
+    for (int l = 0; l < (A::NP1 + NT - 1) / NT; ++l) {
+      const int e = l * NT + tid;
+      if (e < A::NP1) {
+        const int r = e / GE, g = e - r * GE;
+        T w[20];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+          const Q4<T> v = ldsq(stg + r * WI + 4 * (g + u));
+#pragma unroll
+          for (int m = 0; m < 4; ++m) w[4 * u + m] = v.v[m];
+        }
+        Q4<T> o;
+        const int col = e0 + 4 * g;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          T acc = T(0);
+#pragma unroll
+          for (int t = 0; t < KT; ++t) acc += PCS_HH(t) * w[SH1 + m + (KT - 1 - t)];
+          o.v[m] = (unsigned)(col + m) < (unsigned)n2 ? acc : T(0);
+        }
+        int slot = base + r;
+        slot = slot >= RING ? slot - RING : slot;
+        stq(ringA + slot * WE + 4 * g, o);
+      }
+    }
+    lds_barrier();
+    // ---- P2: vertical conv, P2 row (rel. L1 - o1) s RS + r reads ring A rows s RS + r - t
+    if (tid < NV) {
+      Q4<T> acc[RB];
+      vert_pass<T, RB, false>(ringA, base, RB * vrb, vq, hv, acc);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int row = cur.a - (KT - 1) - o1 + cur.s * RS + RB * vrb + r;  // image row of this P2 output
+        if ((unsigned)row >= (unsigned)n1) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[r].v[m] = T(0);
+        }
+        int slot = base + RB * vrb + r;
+        slot = slot >= RING ? slot - RING : slot;
+        stq(ringB + slot * WE + 4 * vq, acc[r]);
+      }
+    }
+    lds_barrier();
+    // ---- P3: vertical correlation (taps hv[14 - t], offset 14 - o1): P3 row s RS + r (rel.
+    // a - 28) reads ring B rows s RS + r - t -> P3 rows in the staging buffer (pitch WE)
+    if (tid < NV) {
+      Q4<T> acc[RB];
+      vert_pass<T, RB, true>(ringB, base, RB * vrb, vq, hv, acc);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) stq(stg + (RB * vrb + r) * WE + 4 * vq, acc[r]);
+    }
+    lds_barrier();
+    // ---- P4: horizontal correlation (taps hh[14 - t], offset 14 - o2) -> output row
+    // a - 28 + s RS + r, columns c0 + 4 g .. + 3
+    {
+      T* dst = out + cur.plane * (int64_t)n1 * n2;
+#pragma unroll 1
+      for (int l = 0; l < (A::NP4 + NT - 1) / NT; ++l) {
+        const int e = l * NT + tid;
+        if (e < A::NP4) {
+          const int r = e / A::GX, g = e - r * A::GX;
+          const int row = cur.a - 2 * (KT - 1) + cur.s * RS + r, gc = c0 + 4 * g;
+          T w[20];
+#pragma unroll
+          for (int u = 0; u < 5; ++u) {
+            const Q4<T> v = ldsq(stg + r * WE + 4 * (g + u));
+#pragma unroll
+            for (int m = 0; m < 4; ++m) w[4 * u + m] = v.v[m];
+          }
+          Q4<T> o;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            T acc = T(0);
+#pragma unroll
+            for (int s = 0; s < KT; ++s) acc += PCS_HH(s) * w[SH4 + m + s];
+            o.v[m] = acc;
+          }
+          if (row >= cur.a && row < cur.b && gc < n2) stq(dst + (int64_t)row * n2 + gc, o);
+        }
+      }
+    }
+    if (!more) break;
+    cur = nxt;
+  }
+#undef PCS_HH
+}
+
+template <typename T>
+static size_t ata_lds_bytes() {
+  using A = AtaG;
+  return sizeof(T) * (size_t)(A::RS * A::WI + 2 * A::RING * A::WE + 32);
+}
+
+// the kernel's LDS (> 64 KB) is dynamic: raise the function's limit once per instantiation
+template <typename T, int SH4>
+static void ata_attr() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep2d_ata<T, SH4>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ata_lds_bytes<T>());
+    (void)hipGetLastError();
+    done = true;
+  }
+}
+
+// resident workgroups of k_sep2d_ata<T> on the device (queried once per type)
+template <typename T>
+static int ata_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    const size_t lds = ata_lds_bytes<T>();
+    ata_attr<T, 1>();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_ata<T, 1>, AtaG::NT, lds) != hipSuccess || nb < 1)
+      nb = 1;
+    (void)hipGetLastError();
+    slots = cus * nb;
+    const char* e = getenv("PCS_ATA_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
+  }
+  return slots;
+}
+
+// horizontal tap padding that makes both horizontal windows fit the strip layout: the padded
+// offset o2 = offb + pad must satisfy o2 % 4 != 1 (SH4 = (-o2) mod 4 <= 2); -1 if none exists
+static int ata_padb(int kb, int offb) {
+  for (int pad = 0; pad <= AtaG::KT - kb; ++pad)
+    if ((offb + pad) % 4 != 1) return pad;
+  return -1;
+}
+
+template <typename T>
+static int sep_ata(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
+                   const void* hb, int kb, int offb, hipStream_t st) {
+  using A = AtaG;
+  if (!in || !out || !ha || !hb || np < 0 || n1 < 1 || n2 < 1 || ka < 1 || ka > A::KT || kb < 1 || kb > A::KT ||
+      offa < 0 || offa >= ka || offb < 0 || offb >= kb || in == out)
+    return PCS_EINVAL;
+  if ((uintptr_t)in % 16 || (uintptr_t)out % 16) return PCS_EINVAL;
+  const int padb = ata_padb(kb, offb);
+  if (padb < 0 || n2 % 4 != 0 || n1 >= (1LL << 30) || n2 >= (1LL << 30)) return PCS_EUNSUPPORTED;
+  if (np == 0) return PCS_OK;
+  const int o2 = offb + padb, sh4 = (4 - o2 % 4) % 4;
+  const int64_t nstrips = (n2 + A::TX - 1) / A::TX, pieces = np * nstrips;
+  const int64_t slots = ata_slots<T>();
+  // row segments: the count minimising (waves of resident workgroups) x (rows per task + the
+  // 28-row prologue of the two vertical passes), segments of >= 64 rows
+  const int64_t max_seg = n1 / 64 > 1 ? n1 / 64 : 1;
+  int64_t nseg = 1, best = -1;
+  for (int64_t c = 1; c <= max_seg; ++c) {
+    const int64_t len = (n1 + c - 1) / c, waves = (pieces * c + slots - 1) / slots;
+    const int64_t cost = waves * (len + 2 * (A::KT - 1));
+    if (best < 0 || cost < best) {
+      best = cost;
+      nseg = c;
+    }
+  }
+  const int64_t seg_len = (n1 + nseg - 1) / nseg;
+  nseg = (n1 + seg_len - 1) / seg_len;
+  const int64_t ntasks = pieces * nseg;
+  const int64_t grid = ntasks < slots ? ntasks : slots;
+  const size_t lds = ata_lds_bytes<T>();
+  auto go = [&](auto kern) {
+    kern<<<(unsigned)grid, A::NT, lds, st>>>((const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg,
+                                             (int)seg_len, ntasks, (const T*)ha, ka, (const T*)hb, kb, offa, padb, o2);
+  };
+  switch (sh4) {
+    case 0: ata_attr<T, 0>(); go(k_sep2d_ata<T, 0>); break;
+    case 1: ata_attr<T, 1>(); go(k_sep2d_ata<T, 1>); break;
+    default: ata_attr<T, 2>(); go(k_sep2d_ata<T, 2>); break;
+  }
+  return launch_status();
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+extern "C" {
+
+int pcs_conv2d_sep_ata_planes(int dt, const void* in, void* out, int64_t nplanes, int64_t n1, int64_t n2,
+                              const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t st) {
+  if (dt == PCS_F32) return sep_ata<float>(in, out, nplanes, n1, n2, ha, ka, offa, hb, kb, offb, st);
+  if (dt == PCS_F64) return sep_ata<double>(in, out, nplanes, n1, n2, ha, ka, offa, hb, kb, offb, st);
+  return PCS_EINVAL;
+}
+
+}  // extern "C"

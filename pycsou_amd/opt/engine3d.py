@@ -114,6 +114,7 @@ class PDS3DEngine:
         self.fkind = fk
         dev = torch.device('cuda', torch.cuda.current_device())
         self.chain = []
+        self.ata = False
         reach = 0
         if fk == L.PCS_F_GRADBUF:
             for op in spec['chain']:
@@ -157,6 +158,21 @@ class PDS3DEngine:
                 esz = torch.empty(0, dtype=dtype).element_size()
                 self.sep2 = (sorted(c[0] for c in self.inplane) == [1, 2] and all(c[3] <= 15 for c in self.inplane)
                              and (plane * esz) % 16 == 0)
+                # opt-in (PCS_3D_ATA=1): the in-plane normal operator in one launch
+                # (pcs_conv2d_sep_ata_planes).  The axis-0 pass commutes with the in-plane ones, so
+                # g = C0^T (C0 (C12^T C12 x) - C12^T y) with C12^T y formed here once: two
+                # sub-volume passes per iteration instead of three (14 words/voxel, not 16), but
+                # the four-pass kernel is LDS/latency-bound at one fp64 workgroup per CU and
+                # measured slower than the two passes it replaces
+                self.ata = False
+                if self.sep2 and os.environ.get('PCS_3D_ATA', '0') == '1':
+                    (ha, ka, oa), (hb, kb, ob) = self._inplane_ab(False)
+                    rc = self.lib.pcs_conv2d_sep_ata_planes(L.dtcode(self.T[0]), L.ptr(self.T[0]), L.ptr(self.T[1]),
+                                                            0, n1, n2, L.ptr(ha), ka, oa, L.ptr(hb), kb, ob,
+                                                            L.stream())
+                    self.ata = rc == 0
+                if self.ata:
+                    self.gbuf = self.T[1]
             else:
                 # the chain's final buffer is fixed by its length: forward + adjoint passes
                 self.gbuf = self.T[(2 * len(self.chain) - 1) % 2]
@@ -178,7 +194,7 @@ class PDS3DEngine:
         # with a real transport the first advance() of >= 5 iterations times both and keeps
         # the faster (max over ranks), unless PCS_3D_ORDER fixes it
         self._tuned = 'PCS_3D_ORDER' in os.environ or not getattr(comm, 'tunable', False)
-        if fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and self.rows > 2 * self.band:
+        if fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and not self.ata and self.rows > 2 * self.band:
             # g in a buffer of its own: the banded order writes g on the boundary planes while the
             # interior's axis-0 pass still reads the in-plane forward result around them
             self.T.append(torch.empty_like(self.T[0]))
@@ -204,6 +220,9 @@ class PDS3DEngine:
                               device=dev)
         a.ws = self.ws.data_ptr()
         self.base_args = a
+        if self.ata:  # C12^T y on every stored plane (setup, once)
+            self.yb = torch.empty_like(self.yw)
+            self._sep_planes(L.ptr(self.yw), L.ptr(self.yb), self.rows + 2 * hg, self.inplane[::-1], True, L.stream())
         self.args = [self._args_for(p) for p in (0, 1)]
         self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
@@ -226,6 +245,19 @@ class PDS3DEngine:
         L.check(self.lib.pcs_conv1d(self.base_args.dtype, L.ptr(src), L.ptr(dst), 3, L.i64s(self.sub_dims),
                                     int(axis), L.ptr(taps), int(k), int(off), st), 'pcs_conv1d')
 
+    def _inplane_ab(self, flipped):
+        """((taps, k, off) along axis 1, (taps, k, off) along axis 2) of the in-plane passes."""
+        out = {}
+        for axis, h, hf, k, off in self.inplane:
+            out[axis] = (hf, k, k - 1 - off) if flipped else (h, k, off)
+        return out[1], out[2]
+
+    def _ata_planes(self, src, dst, np_, st):
+        """dst = C12^T C12 src on np_ planes (both in-plane convolutions and their adjoints)."""
+        (ha, ka, oa), (hb, kb, ob) = self._inplane_ab(False)
+        L.check(self.lib.pcs_conv2d_sep_ata_planes(self.base_args.dtype, src, dst, np_, self.n1, self.n2, L.ptr(ha), ka,
+                                                   oa, L.ptr(hb), kb, ob, st), 'pcs_conv2d_sep_ata_planes')
+
     def _sep_planes(self, src, dst, np_, ops, flipped, st):
         """Both in-plane passes of `ops` (one along axis 1, one along axis 2) in one launch.  The
         two convolutions commute; the axis-2 pass runs first (the faster kernel order,
@@ -240,6 +272,10 @@ class PDS3DEngine:
     def _gradient_fused0(self, p, st):
         nsub = self.rows + 2 * self.hx
         plane = self.plane
+        if self.ata:
+            self._ata_planes(L.ptr(self.X[p]), L.ptr(self.T[0]), nsub, st)
+            self._g_range(self.hx, min(self.hx + self.rows + 1, nsub), st)
+            return
         cur, j = self.X[p], 0
         if self.sep2:
             dst = self.T[0]
@@ -279,6 +315,9 @@ class PDS3DEngine:
         if j1 <= j0:
             return
         off = j0 * self.plane * src.element_size()
+        if self.ata and not flipped:  # the forward in-plane stage is C12^T C12
+            self._ata_planes(ctypes.c_void_p(src.data_ptr() + off), ctypes.c_void_p(dst.data_ptr() + off), j1 - j0, st)
+            return
         ops = self.inplane[::-1] if flipped else self.inplane
         self._sep_planes(ctypes.c_void_p(src.data_ptr() + off), ctypes.c_void_p(dst.data_ptr() + off), j1 - j0, ops,
                          flipped, st)
@@ -290,6 +329,11 @@ class PDS3DEngine:
         nsub = self.rows + 2 * self.hx
         img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0
         _, h, _, k, off = self.ax0
+        if self.ata:  # C0^T (C0 t - C12^T y) straight into g
+            L.check(self.lib.pcs_conv0_residual_adjoint(self.base_args.dtype, L.ptr(self.T[0]), L.ptr(self.yb),
+                                                        L.ptr(self.gbuf), nsub, self.plane, L.ptr(h), int(k), int(off),
+                                                        img_lo, img_hi, q0, q1, st), 'pcs_conv0_residual_adjoint')
+            return
         L.check(self.lib.pcs_conv0_residual_adjoint(self.base_args.dtype, L.ptr(self.T[0]), L.ptr(self.yw),
                                                     L.ptr(self.T[1]), nsub, self.plane, L.ptr(h), int(k), int(off),
                                                     img_lo, img_hi, q0, q1, st), 'pcs_conv0_residual_adjoint')

@@ -228,6 +228,18 @@ def test_pds3d_fused_matches_reference(name, dtype):
     assert isinstance(pds._engine, PDS3DEngine)
 
 
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+def test_pds3d_ata_opt_in_matches_reference(monkeypatch, dtype):
+    """The opt-in two-pass gradient (PCS_3D_ATA=1: pcs_conv2d_sep_ata_planes + the axis-0 pass
+    against C12^T y) reproduces the reference trajectory like the default three-pass chain."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    monkeypatch.setenv('PCS_3D_ATA', '1')
+    c = pds_case('deconv3d_l21_fwd_24_sep15')
+    pds = build(c, dtype, engine='fused')
+    _check(pds, c, dtype)
+    assert isinstance(pds._engine, PDS3DEngine) and pds._engine.ata
+
+
 def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None):
     """A 3-D TV deconvolution case (separable 15-tap Gaussian along every axis), built like
     the golden cases so tests/cases.oracle_pds can run it."""

@@ -1,0 +1,56 @@
+"""Time the in-plane normal operator C12^T C12 of the 3-D engine: one pcs_conv2d_sep_ata_planes
+launch against the two pcs_conv2d_sep_planes launches (forward, flipped) it replaces, on the C4
+(512^3 f32) and C5 (1024^3 f64) volumes.  HIP events, median of 10 after 3 warm-up launches."""
+import os
+import sys
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pycsou_amd import _lib as L  # noqa: E402
+
+
+def med_ms(fn, n=10):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(n):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    lib = L.load()
+    for n, dt in ((512, torch.float32), (1024, torch.float64)):
+        x = torch.randn(n, n, n, dtype=dt, device='cuda')
+        t, g = torch.empty_like(x), torch.empty_like(x)
+        r = np.arange(15) - 7.0
+        h = np.exp(-0.5 * (r / 2.0) ** 2)
+        h /= h.sum()
+        hd = torch.as_tensor(h, dtype=dt, device='cuda')
+        hf = torch.flip(hd, [0]).contiguous()
+        code, st = L.dtcode(x), L.stream()
+
+        def two():
+            assert lib.pcs_conv2d_sep_planes(code, L.ptr(x), L.ptr(t), n, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7, 0,
+                                             st) == 0
+            assert lib.pcs_conv2d_sep_planes(code, L.ptr(t), L.ptr(g), n, n, n, L.ptr(hf), 15, 7, L.ptr(hf), 15, 7, 0,
+                                             st) == 0
+
+        def one():
+            assert lib.pcs_conv2d_sep_ata_planes(code, L.ptr(x), L.ptr(t), n, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7,
+                                                 st) == 0
+        t2, t1 = med_ms(two), med_ms(one)
+        d = (g - t).abs().max().item() / g.abs().max().item()
+        print(f'{os.environ.get("PCS_LIB_PATH", "default")} n={n} {dt}: two passes {t2:.3f} ms, ata {t1:.3f} ms, '
+              f'max rel diff {d:.2e}', flush=True)
+        del x, t, g
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build a diagnostic variant of the engine: tools/build_var.sh NAME -DFLAG=... ; the library lands in
+# pycsou_amd/lib/var/NAME/libpycsou_hip.so (select it with PCS_LIB_PATH).
+cd "$(dirname "$0")/.." || exit 1
+name=$1; shift
+o=build/var_$name; mkdir -p $o pycsou_amd/lib/var/$name
+pids=()
+for f in pycsou_amd/csrc/*.hip; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -fPIC -std=c++17 -Iinclude "$@" -c $f -o $o/$(basename $f .hip).o &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p || exit 1; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o pycsou_amd/lib/var/$name/libpycsou_hip.so $o/*.o
