@@ -267,6 +267,34 @@ int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t stream);
 int pcs_pds2d_run_persistent(const pcs_pds2d_args* a, int64_t n, void* bar, hipStream_t stream);
 int64_t pcs_grid_bar_bytes(void);
 
+/* One fused PrimalDualSplitting.update_iterand + update_diagnostics (pycsou/opt/proxalgs.py:343-394)
+ * for a 2-D image with a general finite-difference K (single GPU, whole image):
+ *   kkind PCS_K_GRAD_{FORWARD,BACKWARD,CENTERED}: K = Gradient(kind, edge, step)  (diff.py:777-882),
+ *         z = [D0 x; D1 x] (2 N), H = lam*L1 or lam*L21 over the two components;
+ *   kkind PCS_K_LAPLACIAN: K = w0 D2_0 + w1 D2_1 (Laplacian(weights, step, edge), diff.py:885-957),
+ *         z has N elements, H = lam*L1.
+ *   fkind PCS_F_NULL: grad F = 0; PCS_F_DENOISE: grad F = x - g (g holds y); PCS_F_GRADBUF: g.
+ * Same update and partials as pcs_pds2d_step (x_t = prox_G((x - tau g) - tau K^T z), ...); the
+ * stencils are the standalone operators' (pcs_grad_fwd/adj, pcs_lap_fwd/adj) per element.  With
+ * hist/ctrl/ws the last workgroups reduce the partials and run the stopping rule (as
+ * pcs_pds2d_step); else only `partials` ([nblocks][4]) is written. */
+enum { PCS_K_GRAD_FORWARD = 0, PCS_K_GRAD_BACKWARD = 1, PCS_K_GRAD_CENTERED = 2, PCS_K_LAPLACIAN = 3 };
+typedef struct {
+  int dtype, kkind, fkind, hkind, gkind, edge;
+  int64_t n0, n1;
+  double tau, sigma, rho, lam, step0, step1, w0, w1, seg_a, seg_b;
+  const void* x; void* xn; const void* z; void* zn; const void* g;
+  double* partials;
+  void* ctrl;
+  double* hist;
+  void* ws; /* pcs_pds2d_stencil_ws_bytes() bytes, zeroed once before first use */
+} pcs_pds2d_stencil_args;
+int64_t pcs_pds2d_stencil_nblocks(const pcs_pds2d_stencil_args* a);
+int64_t pcs_pds2d_stencil_ws_bytes(const pcs_pds2d_stencil_args* a);
+int pcs_pds2d_stencil_step(const pcs_pds2d_stencil_args* a, hipStream_t stream);
+/* n steps back to back, ping-ponging (x, z) <-> (xn, zn); requires hist/ctrl/ws. */
+int pcs_pds2d_stencil_run(const pcs_pds2d_stencil_args* a, int64_t n, hipStream_t stream);
+
 /* ---------------------------------------------------------------- multi-GPU row slabs
  * Native per-rank loop of the row-slab 2-D PDS (one process per GPU, RCCL over xGMI):
  * GenericIterativeAlgorithm.iterate (pycsou/core/solver.py:55-76) around

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get('PCS_LIB_PATH') or os.path.join(_HERE, 'lib', 'libpycs
 PCS_F32, PCS_F64 = 0, 1
 PCS_FORWARD, PCS_BACKWARD, PCS_CENTERED = 0, 1, 2
 PCS_H_L1, PCS_H_L21 = 0, 1
+PCS_K_GRAD_FORWARD, PCS_K_GRAD_BACKWARD, PCS_K_GRAD_CENTERED, PCS_K_LAPLACIAN = 0, 1, 2, 3
 PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
 PCS_APGD_G_L1 = 3
 PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF = 0, 1, 2, 3
@@ -38,6 +39,16 @@ class PdsArgs(ctypes.Structure):
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp),
                 ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64)]
+
+
+class StencilArgs(ctypes.Structure):
+    """Mirror of pcs_pds2d_stencil_args."""
+    _fields_ = [('dtype', _c_int), ('kkind', _c_int), ('fkind', _c_int), ('hkind', _c_int), ('gkind', _c_int),
+                ('edge', _c_int), ('n0', _c_i64), ('n1', _c_i64),
+                ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl), ('step0', _c_dbl),
+                ('step1', _c_dbl), ('w0', _c_dbl), ('w1', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
+                ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('g', _vp),
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
 
 
 class Pds3Args(ctypes.Structure):
@@ -111,6 +122,10 @@ _SIGS = {
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
+    'pcs_pds2d_stencil_nblocks': (_c_i64, [ctypes.POINTER(StencilArgs)]),
+    'pcs_pds2d_stencil_ws_bytes': (_c_i64, [ctypes.POINTER(StencilArgs)]),
+    'pcs_pds2d_stencil_step': (_c_int, [ctypes.POINTER(StencilArgs), _vp]),
+    'pcs_pds2d_stencil_run': (_c_int, [ctypes.POINTER(StencilArgs), _c_i64, _vp]),
     'pcs_pds2d_run_persistent': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp, _vp]),
     'pcs_grid_bar_bytes': (_c_i64, []),
     'pcs_pds2d_nblocks_bands': (_c_i64, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64]),

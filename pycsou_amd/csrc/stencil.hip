@@ -7,6 +7,7 @@
 // the contiguous axis and re-used through L1/L2.  The per-element operation order follows
 // the NumPy slicing order of PyLops 1.x so that fp64 results agree to the last ulp or two.
 #include "common.hpp"
+#include "stencil.hpp"
 
 namespace pcs {
 
@@ -31,44 +32,16 @@ static bool make_geo(int ndim, const int64_t* dims, Geo3& g) {
 
 __device__ __forceinline__ int64_t coord(const Geo3& g, int64_t p, int a) { return (p / g.s[a]) % g.n[a]; }
 
-// D_a x at p (pylops FirstDerivative._matvec_*)
+// D_a x / D_a^T y at p (stencil.hpp cores with the axis geometry of g)
 template <typename T>
 __device__ __forceinline__ T d1_fwd_at(const T* __restrict__ x, const Geo3& g, int64_t p, int a, T h, int kind,
                                        int edge) {
-  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
-  if (kind == PCS_FORWARD) {
-    return (i < n - 1) ? (x[p + s] - x[p]) / h : T(0);
-  } else if (kind == PCS_BACKWARD) {
-    return (i > 0) ? (x[p] - x[p - s]) / h : T(0);
-  }
-  if (i > 0 && i < n - 1) return (T(0.5) * x[p + s] - T(0.5) * x[p - s]) / h;
-  if (!edge || n < 2) return T(0);
-  return (i == 0) ? (x[p + s] - x[p]) / h : (x[p] - x[p - s]) / h;
+  return d1_fwd_core<T, int64_t>(x, p, g.s[a], coord(g, p, a), g.n[a], h, kind, edge);
 }
-
-// (D_a^T y) at p (pylops FirstDerivative._rmatvec_*), accumulation order of the slicing code.
 template <typename T>
 __device__ __forceinline__ T d1_adj_at(const T* __restrict__ y, const Geo3& g, int64_t p, int a, T h, int kind,
                                        int edge) {
-  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
-  T acc = T(0);
-  if (kind == PCS_FORWARD) {
-    if (i < n - 1) acc -= y[p] / h;
-    if (i > 0) acc += y[p - s] / h;
-  } else if (kind == PCS_BACKWARD) {
-    if (i < n - 1) acc -= y[p + s] / h;
-    if (i > 0) acc += y[p] / h;
-  } else {
-    if (i <= n - 3) acc -= (T(0.5) * y[p + s]) / h;
-    if (i >= 2) acc += (T(0.5) * y[p - s]) / h;
-    if (edge && n >= 2) {
-      if (i == 0) acc -= y[p] / h;
-      if (i == 1) acc += y[p - s] / h;
-      if (i == n - 2) acc -= y[p + s] / h;
-      if (i == n - 1) acc += y[p] / h;
-    }
-  }
-  return acc;
+  return d1_adj_core<T, int64_t>(y, p, g.s[a], coord(g, p, a), g.n[a], h, kind, edge);
 }
 
 template <typename T>
@@ -103,32 +76,14 @@ __global__ void k_grad_adj(const T* __restrict__ z, T* __restrict__ out, Geo3 g,
   }
 }
 
-// SecondDerivative (pylops 1.x) along axis a at p.
+// SecondDerivative (pylops 1.x) along axis a at p, and its adjoint
 template <typename T>
 __device__ __forceinline__ T d2_fwd_at(const T* __restrict__ x, const Geo3& g, int64_t p, int a, T h2, int edge) {
-  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
-  if (i > 0 && i < n - 1) return (x[p + s] - T(2) * x[p] + x[p - s]) / h2;
-  if (!edge || n < 3) return T(0);
-  if (i == 0) return (x[p] - T(2) * x[p + s] + x[p + 2 * s]) / h2;
-  return (x[p - 2 * s] - T(2) * x[p - s] + x[p]) / h2;
+  return d2_fwd_core<T, int64_t>(x, p, g.s[a], coord(g, p, a), g.n[a], h2, edge);
 }
-
 template <typename T>
 __device__ __forceinline__ T d2_adj_at(const T* __restrict__ y, const Geo3& g, int64_t p, int a, T h2, int edge) {
-  const int64_t i = coord(g, p, a), n = g.n[a], s = g.s[a];
-  T acc = T(0);
-  if (i <= n - 3) acc += y[p + s] / h2;
-  if (i >= 1 && i <= n - 2) acc -= (T(2) * y[p]) / h2;
-  if (i >= 2) acc += y[p - s] / h2;
-  if (edge && n >= 3) {
-    if (i == 0) acc += y[p] / h2;
-    if (i == 1) acc -= (T(2) * y[p - s]) / h2;
-    if (i == 2) acc += y[p - 2 * s] / h2;
-    if (i == n - 3) acc += y[p + 2 * s] / h2;
-    if (i == n - 2) acc -= (T(2) * y[p + s]) / h2;
-    if (i == n - 1) acc += y[p] / h2;
-  }
-  return acc;
+  return d2_adj_core<T, int64_t>(y, p, g.s[a], coord(g, p, a), g.n[a], h2, edge);
 }
 
 template <typename T>

@@ -31,7 +31,7 @@ from ..func.base import IndicatorFunctional, NullDifferentiableFunctional, NullP
 from ..func.penalty import L1Norm, L21Norm, SquaredL2Norm
 from ..linop.base import HomothetyMap
 from ..linop.conv import Convolve2DOp
-from ..linop.diff import GradientOp
+from ..linop.diff import GradientOp, LaplacianOp
 
 # images at least this large launch chunks from C instead of replaying a captured graph
 NATIVE_MIN_PIXELS = int(os.environ.get('PCS_NATIVE_MIN_PIXELS', 1 << 20))
@@ -43,6 +43,71 @@ def _half_loss_data(F):
             and isinstance(F.map2, DiffMapShifted) and isinstance(F.map2.map, SquaredL2Norm)
             and not np.isscalar(F.map2.shift)):
         return F.map2.shift
+    return None
+
+
+def _match_g(G, spec):
+    """G = None / NullProximableFunctional / NonNegativeOrthant / Segment -> spec['gkind'], spec['seg']."""
+    if G is None or isinstance(G, NullProximableFunctional):
+        spec['gkind'], spec['seg'] = L.PCS_G_NULL, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'nonneg':
+        spec['gkind'], spec['seg'] = L.PCS_G_NONNEG, (0.0, 1.0)
+    elif isinstance(G, IndicatorFunctional) and G.kind == 'segment':
+        spec['gkind'], spec['seg'] = L.PCS_G_SEGMENT, G.params
+    else:
+        return False
+    return True
+
+
+def _match_h(H, ncomp, N):
+    """H = lam * (L1Norm | L21Norm over the ncomp components of each pixel) -> (hkind, lam) or None."""
+    base, lam = H, 1.0
+    if isinstance(H, ProxFuncPostComp):
+        if H.shift != 0:
+            return None
+        base, lam = H.prox_func, float(H.scale)
+    if ncomp > 1 and isinstance(base, L21Norm) and base.pixel_d == ncomp and base.dim == ncomp * N:
+        return L.PCS_H_L21, lam
+    if isinstance(base, L1Norm) and base.dim == ncomp * N:
+        return L.PCS_H_L1, lam
+    return None
+
+
+def match_stencil2d(F, G, H, K, has_H):
+    """Engine spec for the general-stencil fused step (pcs_pds2d_stencil_step): K a 2-D Gradient of
+    any kind (pycsou/linop/diff.py:777-882) or a 2-D Laplacian (diff.py:885-957), H = lam * L1 / L21,
+    F = 0, (1/2) SquaredL2Loss(y), or (1/2) SquaredL2Loss(y) * Convolve2D (grad F through the
+    correlation kernel into a buffer); None otherwise."""
+    if not has_H:
+        return None
+    if isinstance(K, GradientOp) and len(K.dims) == 2:
+        kk, ncomp, w = {'forward': L.PCS_K_GRAD_FORWARD, 'backward': L.PCS_K_GRAD_BACKWARD,
+                        'centered': L.PCS_K_GRAD_CENTERED}[K.kind], 2, (1.0, 1.0)
+    elif isinstance(K, LaplacianOp) and len(K.dims) == 2:
+        kk, ncomp, w = L.PCS_K_LAPLACIAN, 1, tuple(K.weights)
+    else:
+        return None
+    shape = tuple(K.dims)
+    N = shape[0] * shape[1]
+    hm = _match_h(H, ncomp, N)
+    if hm is None:
+        return None
+    spec = {'stencil': True, 'shape': shape, 'steps': tuple(K.steps), 'kkind': kk, 'ncomp': ncomp,
+            'weights': w, 'edge': bool(K.edge), 'hkind': hm[0], 'lam': hm[1]}
+    if not _match_g(G, spec):
+        return None
+    if F is None or isinstance(F, NullDifferentiableFunctional):
+        spec['fkind'] = L.PCS_F_NULL
+        return spec
+    s = _half_loss_data(F)
+    if s is not None and O.numel(s) == N:
+        spec['fkind'], spec['shift'] = L.PCS_F_DENOISE, s
+        return spec
+    if isinstance(F, DiffMapComp) and isinstance(F.map2, Convolve2DOp) and F.map2.dims == shape:
+        s = _half_loss_data(F.map1)
+        if s is not None and O.numel(s) == N:
+            spec['fkind'], spec['shift'], spec['conv'] = L.PCS_F_GRADBUF, s, F.map2
+            return spec
     return None
 
 
@@ -66,14 +131,7 @@ def match_pds2d(F, G, H, K, has_H):
     else:
         return None
     spec['lam'] = lam
-    # G
-    if G is None or isinstance(G, NullProximableFunctional):
-        spec['gkind'], spec['seg'] = L.PCS_G_NULL, (0.0, 1.0)
-    elif isinstance(G, IndicatorFunctional) and G.kind == 'nonneg':
-        spec['gkind'], spec['seg'] = L.PCS_G_NONNEG, (0.0, 1.0)
-    elif isinstance(G, IndicatorFunctional) and G.kind == 'segment':
-        spec['gkind'], spec['seg'] = L.PCS_G_SEGMENT, G.params
-    else:
+    if not _match_g(G, spec):
         return None
     # F
     if F is None or isinstance(F, NullDifferentiableFunctional):
@@ -165,6 +223,13 @@ class PDS2DEngine:
         if self.persistent:
             self.bar = torch.zeros(int(self.lib.pcs_grid_bar_bytes()) // 4, dtype=torch.int32, device=dev)
 
+    # the fused step / the chunk of n steps launched back to back from C, on self.args
+    def _step_call(self, st):
+        L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args), st), 'pcs_pds2d_step')
+
+    def _run_call(self, n):
+        L.check(self.lib.pcs_pds2d_run(ctypes.byref(self.args), int(n), L.stream()), 'pcs_pds2d_run')
+
     # one iteration with parity p (reads buffers p, writes 1-p)
     def _iteration(self, p, hist):
         a, lib, st = self.args, self.lib, L.stream()
@@ -173,7 +238,7 @@ class PDS2DEngine:
         a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
         a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
         a.hist = hist.data_ptr() if self.fused_finalize else None
-        L.check(lib.pcs_pds2d_step(ctypes.byref(a), st), 'pcs_pds2d_step')
+        self._step_call(st)
         if not self.fused_finalize:
             L.check(lib.pcs_pds_reduce_finalize(L.ptr(self.partials), self.nblocks, L.ptr(self.ctrl), L.ptr(hist),
                                                 st), 'pcs_pds_reduce_finalize')
@@ -212,7 +277,7 @@ class PDS2DEngine:
             if rc != -3:
                 L.check(rc, 'pcs_pds2d_run_persistent')
             self.persistent = False  # not applicable to this problem
-        L.check(self.lib.pcs_pds2d_run(ctypes.byref(a), self.chunk, L.stream()), 'pcs_pds2d_run')
+        self._run_call(self.chunk)
 
     def barrier_timed_out(self):
         """True if a persistent launch's grid barrier gave up (grid not co-resident)."""
@@ -252,7 +317,7 @@ class PDS2DEngine:
             a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
             a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
             a.hist = self.hist.data_ptr()
-            L.check(self.lib.pcs_pds2d_run(ctypes.byref(a), int(n), L.stream()), 'pcs_pds2d_run')
+            self._run_call(int(n))
             self._fixed_p = p ^ (int(n) & 1)
             return
         while n >= self.chunk and p == 0:
@@ -296,7 +361,7 @@ class PDS2DEngine:
             a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
             a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
             a.hist = self.hist.data_ptr()
-            timed('step', lambda: L.check(lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step'))
+            timed('step', lambda: self._step_call(L.stream()))
         torch.cuda.synchronize()
         return {k: float(np.median([s.elapsed_time(e) for s, e in v])) for k, v in ev.items()}
 
@@ -318,7 +383,7 @@ class PDS2DEngine:
             a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
             a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
             evs[i][0].record(st)
-            L.check(self.lib.pcs_pds2d_step(ctypes.byref(a), L.stream()), 'pcs_pds2d_step')
+            self._step_call(L.stream())
             evs[i][1].record(st)
         torch.cuda.synchronize()
         a.ctrl, a.hist = ctrl, hist
@@ -372,3 +437,65 @@ class PDS2DEngine:
         n = int(c[0])
         h = hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
         return n, self.X[n % 2], self.Z[n % 2], h
+
+
+class PDS2DStencilEngine(PDS2DEngine):
+    """Device state + loop of the general-stencil fused step (pcs_pds2d_stencil_step): the same
+    loop machinery as PDS2DEngine (device stop flag, chunks launched from C for large images,
+    hipGraph replay otherwise, GRADBUF convolutions before the step), another step kernel."""
+
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, chunk=32, use_graph=True):
+        self.lib = L.gpu()
+        self.spec = spec
+        self.dtype = dtype
+        n0, n1 = spec['shape']
+        self.N = N = n0 * n1
+        nc = spec['ncomp']
+        dev = x0.device
+        self.X = [x0.to(dtype).clone(), torch.empty(N, dtype=dtype, device=dev)]
+        self.Z = [z0.to(dtype).clone(), torch.empty(nc * N, dtype=dtype, device=dev)]
+        self.chunk = max(2, chunk + (chunk % 2))
+        self.use_graph = use_graph
+        a = L.StencilArgs()
+        a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+        a.kkind, a.hkind, a.gkind, a.edge = spec['kkind'], spec['hkind'], spec['gkind'], int(spec['edge'])
+        a.n0, a.n1 = n0, n1
+        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+        a.step0, a.step1 = spec['steps']
+        a.w0, a.w1 = spec['weights']
+        a.seg_a, a.seg_b = spec['seg']
+        fk = spec['fkind']
+        self.conv = None
+        if fk in (L.PCS_F_DENOISE, L.PCS_F_GRADBUF):
+            self.y = -O.to_dev(spec['shift'], dtype)  # y = -shift exactly
+            a.g = self.y.data_ptr()
+        if fk == L.PCS_F_GRADBUF:
+            conv = self.conv = spec['conv']
+            conv._h.get(dtype), conv._hf.get(dtype)
+            self.plans = (conv.plan(dtype, False), conv.plan(dtype, True))
+            self.R = torch.empty(N, dtype=dtype, device=dev)
+            self.Gb = torch.empty(N, dtype=dtype, device=dev)
+            a.g = self.Gb.data_ptr()
+        a.fkind = self.fkind = fk
+        self.args = a
+        self.nblocks = int(self.lib.pcs_pds2d_stencil_nblocks(ctypes.byref(a)))
+        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+        a.partials = self.partials.data_ptr()
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
+        a.ctrl = self.ctrl.data_ptr()
+        self.fused_finalize = True
+        self.ws = torch.zeros(int(self.lib.pcs_pds2d_stencil_ws_bytes(ctypes.byref(a))) // 8 + 2,
+                              dtype=torch.float64, device=dev)
+        a.ws = self.ws.data_ptr()
+        self.graph = None
+        self.hist = None
+        self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
+        self.persistent = False
+        self.bar = None
+
+    def _step_call(self, st):
+        L.check(self.lib.pcs_pds2d_stencil_step(ctypes.byref(self.args), st), 'pcs_pds2d_stencil_step')
+
+    def _run_call(self, n):
+        L.check(self.lib.pcs_pds2d_stencil_run(ctypes.byref(self.args), int(n), L.stream()), 'pcs_pds2d_stencil_run')
