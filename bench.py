@@ -24,7 +24,8 @@ without it.
 
 Single-GPU 2-D legs in the same line (`c2`: BASELINE configs[1], 2048^2 fp32 TV denoising;
 `c3_nonsep`: the C3 problem with a non-separable 15x15 PSF through the register-blocked
-correlation kernel), each with its own roofline.  The operator norms of the single-GPU 2-D
+correlation kernel; `c2_lap` / `c2_cen`: 2048^2 denoising with a Laplacian / centered-Gradient K
+on the general-stencil fused step), each with its own roofline.  The operator norms of the single-GPU 2-D
 problems come from compute_lipschitz_cst() (device Lanczos, untimed setup) as in a reference
 script; the multi-GPU and volume problems use the closed forms (documented in the line).
 
@@ -127,6 +128,35 @@ def build_denoise(n, dtype, seed=0, lipschitz='lanczos'):
     H = 0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2))
     return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
                z0=torch.zeros(2 * N, dtype=dtype, device='cuda'), verbose=None)
+
+
+def build_denoise_k(n, dtype, kind, seed=0, lipschitz='lanczos'):
+    """2-D denoising n x n fp32 with a non-forward K through the general-stencil fused step:
+    kind 'lap': K = Laplacian(edge=True), H = 0.1 * L1Norm (one component per pixel);
+    kind 'centered': K = Gradient(kind='centered', edge=True) (the reference's default Gradient),
+    H = 0.1 * L21Norm (isotropic TV).  ||K|| from compute_lipschitz_cst() (device Lanczos) as a
+    reference script does, or the closed-form bounds (8, 2) with lipschitz='analytic'."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L1Norm, L21Norm
+    from pycsou_amd.linop.diff import Gradient, Laplacian
+    from pycsou_amd.opt.proxalgs import PDS
+    N = n * n
+    xs = torch.as_tensor(phantom((n, n), 64, seed).ravel()).to('cuda', dtype)
+    g = torch.Generator(device='cuda').manual_seed(seed + 1)
+    y = xs + 0.1 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
+    if kind == 'lap':
+        K = Laplacian(shape=(n, n), edge=True)
+        H, hdim = 0.1 * L1Norm(dim=N), N
+    else:
+        K = Gradient(shape=(n, n), kind='centered', edge=True)
+        H, hdim = 0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)), 2 * N
+    if lipschitz == 'lanczos':
+        K.compute_lipschitz_cst()
+    else:
+        K.lipschitz_cst = K.diff_lipschitz_cst = 8.0 if kind == 'lap' else 2.0
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y)
+    return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+               z0=torch.zeros(hdim, dtype=dtype, device='cuda'), verbose=None)
 
 
 def cpu_baseline(n, iters):
@@ -279,10 +309,11 @@ def fused_2d(pds, dtype, K, W, chunk=32):
     """Exactly W untimed then K timed iterations of a fused 2-D problem (PDS2DEngine, fixed
     count); HIP events on the launch stream bracket the K iterations.  Returns ms per
     iteration, the isolated per-kernel launch means and the engine facts."""
-    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.opt.engine import PDS2DEngine, PDS2DStencilEngine
     spec = pds._fused_spec()
     assert spec is not None, 'problem must take the fused 2-D engine'
-    eng = PDS2DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    eng = (PDS2DStencilEngine if spec.get('stencil') else PDS2DEngine)(spec, dtype, pds.tau, pds.sigma, pds.rho,
+                                                                       pds.x0, pds.z0)
     total = W + K + 4
     eng.prepare_fixed(max(total, 4000), chunk)
     spin_up_fixed(eng)
@@ -325,6 +356,38 @@ def leg_c2(args, dtype, K, W):
             'roofline': {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_pt<DENOISE,L21>)', 'kernel_ms': round(km, 5),
                          'achieved': round(alg / (km * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def _leg_stencil(args, dtype, K, W, kind):
+    n = 2048
+    pds = build_denoise_k(n, dtype, kind, lipschitz=args.lipschitz)
+    r = fused_2d(pds, dtype, K, W)
+    del pds
+    elem = 4 if dtype == torch.float32 else 8
+    words = 5 if kind == 'lap' else 7  # read x, y, z (1 or 2 components); write x', z'
+    alg = words * n * n * elem
+    km = r['kernels_ms']['step']
+    kdesc = 'Laplacian(edge=True), 0.1*L1Norm' if kind == 'lap' else 'Gradient(kind=centered, edge=True), 0.1*L21Norm'
+    return {'workload': f'2-D denoising {n}x{n} {args.dtype}, K = {kdesc}, PDS fused general-stencil step '
+                        f'(pcs_pds2d_stencil_step, 32x64 tiles), iterations launched back to back from C',
+            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg,
+            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'roofline': {'bound': 'hbm', 'kernel': f'pcs_pds2d_stencil_step (k_pds2d_gen<float,{kind}>)',
+                         'kernel_ms': round(km, 5), 'achieved': round(alg / (km * 1e-3) / 1e9, 1),
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def leg_c2_lap(args, dtype, K, W):
+    """2048^2 fp32 denoising with K = Laplacian (north_star's second operator family) on the
+    general-stencil fused step: 5 N words per iteration."""
+    return _leg_stencil(args, dtype, K, W, 'lap')
+
+
+def leg_c2_cen(args, dtype, K, W):
+    """2048^2 fp32 TV denoising with the reference's default Gradient (kind='centered',
+    edge=True) on the general-stencil fused step: 7 N words per iteration."""
+    return _leg_stencil(args, dtype, K, W, 'centered')
 
 
 def leg_c3_nonsep(args, dtype, K, W):
@@ -416,9 +479,9 @@ def main():
     ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
                     help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
-    ap.add_argument('--legs', default='c2,c3_nonsep',
+    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen',
                     help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
-                         'PSF); "" skips them')
+                         'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K); "" skips them')
     ap.add_argument('--lipschitz', default='lanczos', choices=['lanczos', 'analytic'],
                     help='operator norms of the single-GPU 2-D problems: compute_lipschitz_cst() or closed forms')
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
@@ -508,7 +571,7 @@ def main():
             out['cpu_baseline'] = None
         if world == 1 and args.engine != 'slab':
             for leg in filter(None, args.legs.split(',')):
-                fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep}[leg]
+                fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen}[leg]
                 try:
                     out[leg] = fn(args, dtype, K, W)
                 except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own

@@ -37,6 +37,7 @@ struct GenG {
 template <typename T>
 struct GenP {
   T tau, sigma, inv_sigma, rho, omr, t_h, inv_t_h, h0, h1, w0, w1, h20, h21, seg_a, seg_b;
+  T ih0, ih1, ih20, ih21;  // reciprocals for the interior path
 };
 
 struct GenGeo {
@@ -86,29 +87,67 @@ __device__ __forceinline__ T gen_kt(const T* Z, int zcs, int l, int i0, int i1, 
   }
 }
 
-template <typename T, int KK, int FK, bool VEC>
-__global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x, T* __restrict__ xn,
-                                                         const T* __restrict__ z, T* __restrict__ zn,
-                                                         const T* __restrict__ gsrc, GenGeo geo, GenP<T> P, int hk,
-                                                         int gk, double* __restrict__ partials, Ctrl* ctrl,
-                                                         double* hist, void* ws, int ntasks) {
+// Interior stencils (every pixel of the U region and the tile at >= 2 samples from the image
+// edges, i.e. no edge rule can apply): branch-free, 1/h as a multiplication (exact for unit steps).
+template <typename T, int KK>
+__device__ __forceinline__ T gen_kt_int(const T* Z, int zcs, int l, const GenP<T>& P) {
+  constexpr int CW = GenG::CW;
+  if constexpr (KK == KK_LAP) {
+    T a0 = Z[l + CW] * P.ih20;
+    a0 -= (T(2) * Z[l]) * P.ih20;
+    a0 += Z[l - CW] * P.ih20;
+    T a1 = Z[l + 1] * P.ih21;
+    a1 -= (T(2) * Z[l]) * P.ih21;
+    a1 += Z[l - 1] * P.ih21;
+    return P.w0 * a0 + P.w1 * a1;
+  } else {
+    const T* Z1 = Z + zcs;
+    T a0, a1;
+    if constexpr (KK == PCS_FORWARD) {
+      a0 = -(Z[l] * P.ih0) + Z[l - CW] * P.ih0;
+      a1 = -(Z1[l] * P.ih1) + Z1[l - 1] * P.ih1;
+    } else if constexpr (KK == PCS_BACKWARD) {
+      a0 = -(Z[l + CW] * P.ih0) + Z[l] * P.ih0;
+      a1 = -(Z1[l + 1] * P.ih1) + Z1[l] * P.ih1;
+    } else {
+      a0 = -((T(0.5) * Z[l + CW]) * P.ih0) + (T(0.5) * Z[l - CW]) * P.ih0;
+      a1 = -((T(0.5) * Z1[l + 1]) * P.ih1) + (T(0.5) * Z1[l - 1]) * P.ih1;
+    }
+    return (T(0) + a0) + a1;
+  }
+}
+template <typename T, int KK>
+__device__ __forceinline__ void gen_ku_int(const T* U, int l, const GenP<T>& P, T* ku) {
+  constexpr int CW = GenG::CW;
+  if constexpr (KK == KK_LAP) {
+    ku[0] = P.w0 * ((U[l + CW] - T(2) * U[l] + U[l - CW]) * P.ih20) + P.w1 * ((U[l + 1] - T(2) * U[l] + U[l - 1]) * P.ih21);
+  } else if constexpr (KK == PCS_FORWARD) {
+    ku[0] = (U[l + CW] - U[l]) * P.ih0;
+    ku[1] = (U[l + 1] - U[l]) * P.ih1;
+  } else if constexpr (KK == PCS_BACKWARD) {
+    ku[0] = (U[l] - U[l - CW]) * P.ih0;
+    ku[1] = (U[l] - U[l - 1]) * P.ih1;
+  } else {
+    ku[0] = (T(0.5) * U[l + CW] - T(0.5) * U[l - CW]) * P.ih0;
+    ku[1] = (T(0.5) * U[l + 1] - T(0.5) * U[l - 1]) * P.ih1;
+  }
+}
+
+template <typename T, int KK, int FK, bool VEC, bool INT>
+__device__ __forceinline__ void gen_tile(const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z,
+                                         T* __restrict__ zn, const T* __restrict__ gsrc, const GenGeo& geo,
+                                         const GenP<T>& P, int hk, int gk, int r0, int c0, T* Z, T* U,
+                                         double (&part)[4]) {
   using G = GenG;
   constexpr int D = (KK == KK_LAP) ? 1 : 2, CW = G::CW, CG = G::CG, NT = G::NT, ZS = G::ZR * G::CW;
-  __shared__ __attribute__((aligned(16))) T Z[D * ZS];
-  __shared__ __attribute__((aligned(16))) T U[G::UR * G::CW];
-  __shared__ double red[4 * (G::NT / 64)];
-  __shared__ int flag[2];
-  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
-  int task;
-  {  // XCD-aware bijective remap: consecutive tiles of a row share an XCD (their halo lines)
-    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
-    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
-  }
-  const int ty = task / geo.tiles1, tx = task - ty * geo.tiles1;
-  const int r0 = ty * G::TR, c0 = tx * G::TC;
+  constexpr bool LV = VEC || INT;  // interior tiles: every group of the regions is inside the image
   const int n0 = geo.n0, n1 = geo.n1, edge = geo.edge;
   const int64_t N = (int64_t)n0 * n1;
   const int tid = threadIdx.x;
+  auto ld = [&](const T* a, int r, int c) -> G4<T> {
+    if constexpr (INT && VEC) return ld4(a + (int64_t)r * n1 + c);
+    else return gen_ld4<T, LV && VEC>(a, n0, n1, r, c);
+  };
 
   // ---- loads: z region -> registers -> LDS; x (and g) of the U items -> registers
   G4<T> xr[G::KU], gr[G::KU];
@@ -119,13 +158,13 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
 #pragma unroll
       for (int k = 0; k < G::KZ; ++k) {
         const int e = min(k * NT + tid, G::NZI - 1), rr = e / CG, g = e - rr * CG;
-        zr[d][k] = gen_ld4<T, VEC>(z + d * N, n0, n1, r0 - 4 + rr, c0 - 4 + 4 * g);
+        zr[d][k] = ld(z + d * N, r0 - 4 + rr, c0 - 4 + 4 * g);
       }
 #pragma unroll
     for (int k = 0; k < G::KU; ++k) {
       const int e = min(k * NT + tid, G::NUI - 1), rr = e / CG, g = e - rr * CG;
-      xr[k] = gen_ld4<T, VEC>(x, n0, n1, r0 - 2 + rr, c0 - 4 + 4 * g);
-      if constexpr (FK != PCS_F_NULL) gr[k] = gen_ld4<T, VEC>(gsrc, n0, n1, r0 - 2 + rr, c0 - 4 + 4 * g);
+      xr[k] = ld(x, r0 - 2 + rr, c0 - 4 + 4 * g);
+      if constexpr (FK != PCS_F_NULL) gr[k] = ld(gsrc, r0 - 2 + rr, c0 - 4 + 4 * g);
     }
 #pragma unroll
     for (int d = 0; d < D; ++d)
@@ -136,7 +175,6 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
       }
   }
   __syncthreads();
-  double part[4] = {0.0, 0.0, 0.0, 0.0};
   // ---- U items: x_t, u on rows [r0 - 2, r0 + TR + 2) x columns [c0 - 2, c0 + TC + 2); x' on the tile
 #pragma unroll
   for (int k = 0; k < G::KU; ++k) {
@@ -151,22 +189,25 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int i1 = cb + m;
-        const bool in = (unsigned)i0 < (unsigned)n0 && (unsigned)i1 < (unsigned)n1 && i1 >= c0 - 2 &&
-                        i1 < c0 + G::TC + 2;
-        T u = T(0), xnew = T(0);
+        // interior tiles: every column of the item is in the image (the two outside the U region
+        // compute unused values from in-bounds LDS neighbours)
+        const bool in = INT || ((unsigned)i0 < (unsigned)n0 && (unsigned)i1 < (unsigned)n1 && i1 >= c0 - 2 &&
+                                i1 < c0 + G::TC + 2);
+        T u = T(0), xnew = T(0), xv = xr[k].v[m];
         if (in) {
-          const T xv = xr[k].v[m];
           T gf = T(0);
           if constexpr (FK == PCS_F_DENOISE) gf = xv - gr[k].v[m];  // (2 (x + (-y))) 0.5, exact
           else if constexpr (FK == PCS_F_GRADBUF) gf = gr[k].v[m];
-          const T kt = gen_kt<T, KK>(Z, ZS, lz + m, i0, i1, n0, n1, P, edge);
+          T kt;
+          if constexpr (INT) kt = gen_kt_int<T, KK>(Z, ZS, lz + m, P);
+          else kt = gen_kt<T, KK>(Z, ZS, lz + m, i0, i1, n0, n1, P, edge);
           const T xt = prox_g((xv - P.tau * gf) - P.tau * kt, gk, P.seg_a, P.seg_b);
           u = T(2) * xt - xv;
           xnew = P.rho * xt + P.omr * xv;
-          const T dx = xv - xnew;
-          sdx += dx * dx;
-          sx += xv * xv;
         }
+        const T dx = xv - xnew;
+        sdx += (in && i1 < n1) ? dx * dx : T(0);
+        sx += (in && i1 < n1) ? xv * xv : T(0);
         uo.v[m] = u;
         xo.v[m] = xnew;
       }
@@ -174,7 +215,7 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
       if (own) {
         part[0] += (double)sdx;
         part[1] += (double)sx;
-        gen_st4<T, VEC>(xn, n1, i0, cb, xo);
+        gen_st4<T, LV && VEC>(xn, n1, i0, cb, xo);
       }
     }
   }
@@ -186,7 +227,7 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
     if (e < G::NOI) {
       const int rr = e / (G::TC / 4), g = e - rr * (G::TC / 4);
       const int i0 = r0 + rr, cb = c0 + 4 * g;
-      if (i0 < n0 && cb < n1) {
+      if (INT || (i0 < n0 && cb < n1)) {
         const int lu = (rr + 2) * CW + 4 * (g + 1), lz = (rr + 4) * CW + 4 * (g + 1);
         G4<T> o[D];
         T sdz = T(0), sz = T(0);
@@ -194,7 +235,9 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
         for (int m = 0; m < 4; ++m) {
           const int i1 = cb + m;
           T ku[D], zv[D];
-          if constexpr (KK == KK_LAP) {  // w0 D2_0 u + w1 D2_1 u (pylops Laplacian matvec)
+          if constexpr (INT) {
+            gen_ku_int<T, KK>(U, lu + m, P, ku);
+          } else if constexpr (KK == KK_LAP) {  // w0 D2_0 u + w1 D2_1 u (pylops Laplacian matvec)
             ku[0] = P.w0 * d2_fwd_core<T, int>(U, lu + m, CW, i0, n0, P.h20, edge) +
                     P.w1 * d2_fwd_core<T, int>(U, lu + m, 1, i1, n1, P.h21, edge);
           } else {
@@ -217,7 +260,7 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
 #pragma unroll
             for (int d = 0; d < D; ++d) zt[d] = w[d] - P.sigma * (v[d] - P.t_h * clip1(v[d] * P.inv_t_h));
           }
-          const bool cm = i1 < n1;
+          const bool cm = INT || i1 < n1;
 #pragma unroll
           for (int d = 0; d < D; ++d) {
             o[d].v[m] = P.rho * zt[d] + P.omr * zv[d];
@@ -229,10 +272,40 @@ __global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x,
         part[2] += (double)sdz;
         part[3] += (double)sz;
 #pragma unroll
-        for (int d = 0; d < D; ++d) gen_st4<T, VEC>(zn + d * N, n1, i0, cb, o[d]);
+        for (int d = 0; d < D; ++d) gen_st4<T, LV && VEC>(zn + d * N, n1, i0, cb, o[d]);
       }
     }
   }
+}
+
+template <typename T, int KK, int FK, bool VEC>
+__global__ __launch_bounds__(GenG::NT) void k_pds2d_gen(const T* __restrict__ x, T* __restrict__ xn,
+                                                         const T* __restrict__ z, T* __restrict__ zn,
+                                                         const T* __restrict__ gsrc, GenGeo geo, GenP<T> P, int hk,
+                                                         int gk, double* __restrict__ partials, Ctrl* ctrl,
+                                                         double* hist, void* ws, int ntasks) {
+  using G = GenG;
+  constexpr int D = (KK == KK_LAP) ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) T Z[D * G::ZR * G::CW];
+  __shared__ __attribute__((aligned(16))) T U[G::UR * G::CW];
+  __shared__ double red[4 * (G::NT / 64)];
+  __shared__ int flag[2];
+  if (ctrl != nullptr && ctrl->stopped != 0) return;  // loop already stopped (solver.py:65-66)
+  int task;
+  {  // XCD-aware bijective remap: consecutive tiles of a row share an XCD (their halo lines)
+    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int ty = task / geo.tiles1, tx = task - ty * geo.tiles1;
+  const int r0 = ty * G::TR, c0 = tx * G::TC;
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  // interior tile (uniform): the U region and the tile are >= 2 samples inside the image and the
+  // regions' loads are all in bounds -> no edge rule, no bounds check
+  const bool interior = r0 >= 4 && r0 + G::TR + 4 <= geo.n0 && c0 >= 4 && c0 + G::TC + 4 <= geo.n1;
+  if (interior)
+    gen_tile<T, KK, FK, VEC, true>(x, xn, z, zn, gsrc, geo, P, hk, gk, r0, c0, Z, U, part);
+  else
+    gen_tile<T, KK, FK, VEC, false>(x, xn, z, zn, gsrc, geo, P, hk, gk, r0, c0, Z, U, part);
   block_sum<4>(part, red);
   if (hist != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
@@ -272,6 +345,10 @@ static int gen_launch(const pcs_pds2d_stencil_args* a, const void* x, void* xn, 
   P.w1 = (T)a->w1;
   P.h20 = (T)(a->step0 * a->step0);
   P.h21 = (T)(a->step1 * a->step1);
+  P.ih0 = (T)(1.0 / a->step0);
+  P.ih1 = (T)(1.0 / a->step1);
+  P.ih20 = (T)(1.0 / (a->step0 * a->step0));
+  P.ih21 = (T)(1.0 / (a->step1 * a->step1));
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
   const int ntasks = (int)gen_tiles(a);
