@@ -326,6 +326,9 @@ typedef struct {
  * (the exchange step of SURVEY 8(e)): send_lo -> rank-1's recv_hi, send_hi -> rank+1's recv_lo.
  * world == 1: no-op.  Graph-capturable (no allocation, no host synchronisation). */
 int pcs_halo_exchange(void* comm, int rank, int world, const pcs_halo_set* h, hipStream_t stream);
+/* dst[r * count .. (r + 1) * count) = src of rank r (RCCL all-gather over `comm` on `stream`; the
+ * norm-sums step of SURVEY 8(e)); comm NULL (world 1 only): a device copy.  Graph-capturable. */
+int pcs_allgather_f64(void* comm, int world, const double* src, double* dst, int64_t count, hipStream_t stream);
 
 typedef struct {
   int world, rank;

@@ -135,6 +135,7 @@ _SIGS = {
     'pcs_comm_unique_id': (_c_int, [_vp]),
     'pcs_comm_init': (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(_vp)]),
     'pcs_comm_destroy': (_c_int, [_vp]),
+    'pcs_allgather_f64': (_c_int, [_vp, _c_int, _vp, _vp, _c_i64, _vp]),
     'pcs_halo_exchange': (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(HaloSet), _vp]),
     'pcs_slab2d_create': (_c_int, [ctypes.POINTER(Slab2DDesc), _vp, ctypes.POINTER(_vp)]),
     'pcs_slab2d_overlapped': (_c_int, [_vp]),

@@ -283,6 +283,19 @@ int pcs_halo_exchange(void* comm, int rank, int world, const pcs_halo_set* h, hi
   return halo_exchange_on((ncclComm_t)comm, rank, world, *h, st);
 }
 
+int pcs_allgather_f64(void* comm, int world, const double* src, double* dst, int64_t count, hipStream_t st) {
+  if (!src || !dst || count < 0 || world < 1) return PCS_EINVAL;
+  if (!comm) {
+    if (world > 1) return PCS_EINVAL;
+    return hipMemcpyAsync(dst, src, (size_t)count * sizeof(double), hipMemcpyDeviceToDevice, st) == hipSuccess
+               ? PCS_OK
+               : PCS_ELAUNCH;
+  }
+  if (!rccl().ok) return PCS_EINVAL;
+  return rccl().all_gather(src, dst, (size_t)count, ncclFloat64, (ncclComm_t)comm, st) == ncclSuccess ? PCS_OK
+                                                                                                    : PCS_ELAUNCH;
+}
+
 int pcs_slab2d_overlapped(const void* plan) { return plan && ((const Slab2DPlan*)plan)->overlap ? 1 : 0; }
 
 int pcs_slab2d_run(void* plan, int64_t n, int p0, hipStream_t st) {

@@ -104,6 +104,15 @@ class PDS3DEngine:
         self.lib = L.gpu()
         self.spec, self.dtype, self.comm = spec, dtype, comm
         self.rank, self.world = int(rank), int(world)
+        # multi-GPU transport: the library's RCCL binding (pcs_halo_exchange / pcs_allgather_f64,
+        # stream-ordered, so a chunk of iterations -- kernels and RCCL -- is captured into one
+        # hipGraph) when the group offers it; PCS_3D_NATIVE=0 keeps the torch.distributed calls
+        self.native_comm = False
+        if (self.world > 1 and comm is not None and hasattr(comm, 'rccl')
+                and os.environ.get('PCS_3D_NATIVE', '1') != '0'):
+            rc = comm.rccl()
+            if rc is not None:
+                self.comm, self.native_comm = rc, True
         n0, n1, n2 = spec['shape']
         self.n0, self.n1, self.n2 = n0, n1, n2
         plane = n1 * n2
@@ -231,7 +240,8 @@ class PDS3DEngine:
         self.hist = None
         self.graph = None
         self.chunk = max(2, chunk + chunk % 2)
-        self.use_graph = use_graph and world == 1
+        # graphs: one GPU, or the native RCCL transport (PCS_3D_GRAPH=0 launches eagerly)
+        self.use_graph = use_graph and (world == 1 or (self.native_comm and os.environ.get('PCS_3D_GRAPH', '1') != '0'))
 
     def _args_for(self, p):
         b = L.Pds3Args()
@@ -484,16 +494,41 @@ class PDS3DEngine:
     def _chunk(self):
         for i in range(self.chunk):
             self.iteration(i % 2)
+        if self.world > 1:
+            self._drain()  # the side stream rejoins before the chunk (and a capture) ends
+
+    def _capture(self):
+        """Capture one chunk into a hipGraph.  Multi-GPU: every rank must end up with a graph or
+        none (the captured RCCL calls pair across ranks), so the outcome is agreed collectively and
+        a failed capture anywhere falls back to eager launches everywhere."""
+        torch.cuda.synchronize()
+        g, ok = torch.cuda.CUDAGraph(), True
+        try:
+            with torch.cuda.graph(g):
+                self._chunk()
+        except RuntimeError:
+            ok, g = False, None
+            self._pending_ex = self._pending_ag = None  # handles of the aborted capture
+            torch.cuda.synchronize()
+        if self.world > 1:
+            flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=self.sums.device)
+            allf = torch.zeros(self.world, dtype=torch.float64, device=self.sums.device)
+            self.comm.allgather(flag, allf)
+            ok = bool(allf.min().item() > 0)
+        if not ok:
+            self.use_graph, g = False, None
+        self.graph = g
+        return ok
 
     def advance(self, k):
         """Enqueue k iterations (k a multiple of the chunk when graphs are used)."""
-        if self.use_graph:
-            if self.graph is None:
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._chunk()
-                self.graph = g
+        if self.use_graph and self.world > 1 and not self._tuned and self.banded and self.overlap and k >= 5:
+            self._autotune()  # eager, before the capture; then back to parity 0 for the graph
+            if self._p == 1:
+                self.iteration(1)
+                self._p = 0
+            self._drain()
+        if self.use_graph and (self.graph is not None or self._capture()):
             for _ in range(k // self.chunk):
                 self.graph.replay()
             return

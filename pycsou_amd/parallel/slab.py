@@ -89,6 +89,12 @@ class DistComm:
             self._native = h
         return self._native or None
 
+    def rccl(self):
+        """The in-library RCCL transport (RcclComm) over the same ranks, or None (host-staged
+        group, one rank, or no RCCL).  Collective."""
+        h = self.native()
+        return RcclComm(h, self.rank, self.world, self) if h else None
+
     def close(self):
         if self._native:
             torch.cuda.synchronize()
@@ -154,6 +160,83 @@ class DistComm:
                 ops.append(dist.P2POp(dist.irecv, r, self._peer(peer), self.group))
         for q in dist.batch_isend_irecv(ops):
             q.wait()
+
+
+class RcclComm:
+    """Halo exchange and sums all-gather through the library's RCCL binding
+    (pcs_halo_exchange / pcs_allgather_f64) instead of torch.distributed: plain
+    stream-ordered launches, so a chunk of iterations (kernels + RCCL) can be captured into one
+    hipGraph.  The *_start forms run on a side stream forked from the current one (event
+    record / wait, capture-safe); the handle's wait() joins it back.  Same interface as
+    DistComm for the engines."""
+
+    tunable = True
+
+    def __init__(self, handle, rank, world, owner=None):
+        self.h, self.rank, self.world, self.owner = handle, int(rank), int(world), owner
+        self.lib = L.gpu()
+        self.side = torch.cuda.Stream()
+        self._sets = {}
+
+    def _halo_set(self, pairs):
+        """pcs_halo_set of {peer: [(send, recv), ...]} (cached per pairs object: the engines
+        build one per ping-pong parity)."""
+        key = id(pairs)
+        hs = self._sets.get(key)
+        if hs is not None and hs[1] is pairs:
+            return hs[0]
+        lo, hi = pairs.get(self.rank - 1, []), pairs.get(self.rank + 1, [])
+        n = max(len(lo), len(hi))
+        if n > 4:
+            raise ValueError('pcs_halo_exchange moves at most 4 buffers')
+        h = L.HaloSet()
+        h.nbuf = n
+        for k in range(n):
+            ref = (lo or hi)[k][0]
+            h.bytes[k] = ref.numel() * ref.element_size()
+            if lo:
+                h.send_lo[k], h.recv_lo[k] = lo[k][0].data_ptr(), lo[k][1].data_ptr()
+            if hi:
+                h.send_hi[k], h.recv_hi[k] = hi[k][0].data_ptr(), hi[k][1].data_ptr()
+        self._sets[key] = (h, pairs)
+        return h
+
+    def allgather(self, src, dst):
+        L.check(self.lib.pcs_allgather_f64(self.h, self.world, L.ptr(src), L.ptr(dst), src.numel(), L.stream()),
+                'pcs_allgather_f64')
+
+    def exchange(self, pairs):
+        if not pairs:
+            return
+        L.check(self.lib.pcs_halo_exchange(self.h, self.rank, self.world, ctypes.byref(self._halo_set(pairs)),
+                                           L.stream()), 'pcs_halo_exchange')
+
+    def _on_side(self, fn):
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            fn()
+        return _SideJoin(self.side)
+
+    def allgather_start(self, src, dst):
+        return self._on_side(lambda: self.allgather(src, dst))
+
+    def exchange_start(self, pairs):
+        return self._on_side(lambda: self.exchange(pairs))
+
+    def close(self):
+        if self.owner is not None:
+            self.owner.close()
+
+
+class _SideJoin:
+    """Handle of work queued on a side stream: wait() orders the current stream after it."""
+
+    def __init__(self, side):
+        self.side = side
+
+    def wait(self):
+        torch.cuda.current_stream().wait_stream(self.side)
 
 
 class _Done:

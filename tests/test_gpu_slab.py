@@ -409,6 +409,46 @@ def test_rccl_binding_world1():
     assert lib.pcs_comm_destroy(h) == 0
 
 
+def test_rccl_transport_graph_capture_world1():
+    """RcclComm (the 3-D engine's multi-GPU transport): the RCCL all-gather of the norm sums
+    through pcs_allgather_f64 on a one-rank communicator, eager, on the side stream
+    (allgather_start / wait) and captured into a hipGraph and replayed -- the capture the
+    multi-GPU 3-D loop relies on."""
+    import ctypes
+    from pycsou_amd import _lib as L
+    from pycsou_amd.parallel.slab import RcclComm
+    lib = L.gpu()
+    nb = int(lib.pcs_comm_id_bytes())
+    uid = (ctypes.c_ubyte * nb)()
+    assert lib.pcs_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)) == 0
+    h = ctypes.c_void_p()
+    assert lib.pcs_comm_init(ctypes.cast(uid, ctypes.c_void_p), 1, 0, ctypes.byref(h)) == 0
+    rc = RcclComm(h, 0, 1)
+    src = torch.arange(4, dtype=torch.float64, device='cuda') + 1.0
+    dst = torch.zeros(4, dtype=torch.float64, device='cuda')
+    rc.allgather(src, dst)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    dst.zero_()
+    rc.allgather_start(src, dst).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        src.mul_(2.0)
+        rc.allgather_start(src, dst).wait()
+        dst.add_(1.0)
+    src.copy_(torch.arange(4, dtype=torch.float64, device='cuda'))
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dst, torch.arange(4, dtype=torch.float64, device='cuda') * 8.0 + 1.0)
+    rc.exchange({})  # no neighbours: nothing to move
+    del g
+    torch.cuda.synchronize()
+    assert lib.pcs_comm_destroy(h) == 0
+
+
 @pytest.mark.parametrize('shape, thr', [((700, 256), 2e-3), ((1100, 1000), 0.0)])
 def test_persistent_loop_matches_launches(monkeypatch, shape, thr):
     """pcs_pds2d_run_persistent (one launch per chunk, a grid barrier per iteration) against

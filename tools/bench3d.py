@@ -128,6 +128,15 @@ class NullComm:
         pass
 
 
+class NullGraphComm(NullComm):
+    """NullComm shaped like the native RCCL transport: stream-ordered only, so the engine
+    captures its chunks into hipGraphs (the multi-GPU path's launch structure)."""
+    staged = False
+
+    def rccl(self):
+        return self
+
+
 def rank_share(args):
     from pycsou_amd.opt.engine3d import PDS3DEngine
     torch.cuda.set_device(0)
@@ -139,14 +148,19 @@ def rank_share(args):
     pds = build(args.size, dtype)
     spec = pds._fused_spec()
     print(f'built in {time.time() - t0:.1f} s', flush=True)
-    K = args.steps + args.steps % 2
+    K = -(-args.steps // 8) * 8  # whole chunks of 8 (the graph variants replay chunks)
     out = {'workload': f'one rank ({rank} of {W}) of 3-D TV-deconv {args.size}^3 {args.dtype}'}
-    for name, ov, order in (('serial', False, 'split'), ('banded', True, 'split'), ('banded_fullg', True, 'fullg')):
-        eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, comm=NullComm(rank, W),
-                          rank=rank, world=W, overlap=ov)
+    runs = [(name + ('_graph' if g else ''), ov, order, g) for g in (False, True)
+            for name, ov, order in (('serial', False, 'split'), ('banded', True, 'split'),
+                                    ('banded_fullg', True, 'fullg'))]
+    for name, ov, order, graph in runs:
+        comm = (NullGraphComm if graph else NullComm)(rank, W)
+        eng = PDS3DEngine(spec, dtype, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, comm=comm,
+                          rank=rank, world=W, overlap=ov, chunk=8)
+        assert eng.use_graph == graph
         eng.order = order
-        eng.init_loop(K + 8, K + 8, -1.0)
-        eng.advance(4)
+        eng.init_loop(K + 16, K + 16, -1.0)
+        eng.advance(8)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
