@@ -30,6 +30,7 @@ of one process (one GPU) with device-to-device halo copies for the parity tests.
 """
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -374,6 +375,12 @@ class SlabPDS2D:
         self.overlap = bool(overlap)
         self._plan = None
         self._plan_key = None
+        # multi-GPU native loop: chunks of 32 iterations replayed from a hipGraph (kernels, events
+        # and RCCL calls; world-1 C3 probe: serial schedule equal, overlapped 0.164 -> 0.158 ms per
+        # iteration, profiles/r2_slab_graph_probe.txt); PCS_SLAB_GRAPH=<even chunk> sets it, 0 = eager
+        gc = int(os.environ.get('PCS_SLAB_GRAPH', '32' if world > 1 else '0') or 0)
+        self.graph_chunk = (gc + gc % 2) if self.native and gc > 0 else 0
+        self._graph = None
 
     @classmethod
     def from_pds(cls, pds, comm, rank=None, world=None, chunk=16, native='auto', overlap=True):
@@ -431,6 +438,7 @@ class SlabPDS2D:
         return h
 
     def _destroy_plan(self):
+        self._graph = None  # captured against this plan's streams, events and buffers
         if self._plan is not None:
             torch.cuda.synchronize()
             L.load().pcs_slab2d_destroy(self._plan)
@@ -506,12 +514,48 @@ class SlabPDS2D:
             if (not getattr(self, '_tuned', False) and self.world > 1 and self.overlap and k >= 8
                     and getattr(self.comm, 'tunable', False)):
                 k -= self._autotune()
-            L.check(self.lib.pcs_slab2d_run(self._native_plan(), int(k), self._p, L.stream()), 'pcs_slab2d_run')
-            self._p ^= int(k) & 1
+            if self.graph_chunk and k >= self.graph_chunk:
+                k = self._replay_graph(k)
+            if k:
+                L.check(self.lib.pcs_slab2d_run(self._native_plan(), int(k), self._p, L.stream()), 'pcs_slab2d_run')
+                self._p ^= int(k) & 1
             return
         for _ in range(k):
             self.iteration(self._p)
             self._p ^= 1
+
+    def _replay_graph(self, k):
+        """PCS_SLAB_GRAPH=<chunk>: the native loop's chunk (kernels, events, RCCL) captured into a
+        hipGraph and replayed; returns the iterations left for eager launches.  Every rank must
+        hold a graph or none (captured RCCL calls pair across ranks): agreed collectively, a
+        failed capture anywhere leaves every rank on the eager native loop."""
+        c = self.graph_chunk
+        if self._p == 1:  # graphs start at parity 0
+            L.check(self.lib.pcs_slab2d_run(self._native_plan(), 1, 1, L.stream()), 'pcs_slab2d_run')
+            self._p, k = 0, k - 1
+        if self._graph is None:
+            plan = self._native_plan()
+            torch.cuda.synchronize()
+            g, ok = torch.cuda.CUDAGraph(), True
+            try:
+                with torch.cuda.graph(g):
+                    L.check(self.lib.pcs_slab2d_run(plan, c, 0, L.stream()), 'pcs_slab2d_run')
+            except RuntimeError:
+                ok, g = False, None
+                torch.cuda.synchronize()
+            if self.world > 1:
+                flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=self.sums.device)
+                allf = torch.zeros(self.world, dtype=torch.float64, device=self.sums.device)
+                self.comm.allgather(flag, allf)
+                ok = bool(allf.min().item() > 0)
+            if not ok:
+                self.graph_chunk = 0
+                return k
+            self._graph = g
+        while k >= c:
+            self._graph.replay()
+            k -= c
+        return k
 
     def _autotune(self):
         """Serial or overlapped native schedule: which is faster depends on the RCCL latency of

@@ -266,6 +266,28 @@ def test_native_loop_world1(kind, overlap):
 
 
 @pytest.mark.parametrize('overlap', [True, False])
+def test_native_loop_graph_world1(monkeypatch, overlap):
+    """PCS_SLAB_GRAPH: the native loop's chunks captured into a hipGraph (kernels, the side
+    stream's events) and replayed, with an eager remainder and an odd start parity: bitwise the
+    eager native loop."""
+    from pycsou_amd.parallel import SlabPDS2D
+    pds = _problem('deconv')
+    spec = pds._fused_spec()
+    s1 = SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, 0, 1, native=True,
+                   overlap=overlap, chunk=7)
+    n1, x1, z1, h1 = s1.run(40, 40, 0.0)
+    monkeypatch.setenv('PCS_SLAB_GRAPH', '6')
+    s2 = SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, 0, 1, native=True,
+                   overlap=overlap, chunk=7)
+    assert s2.graph_chunk == 6
+    n2, x2, z2, h2 = s2.run(40, 40, 0.0)
+    assert s2._graph is not None
+    assert n1 == n2 == 41
+    assert torch.equal(x2, x1) and torch.equal(z2, z1)
+    np.testing.assert_array_equal(h2, h1)
+
+
+@pytest.mark.parametrize('overlap', [True, False])
 def test_native_loop_early_stop(overlap):
     """Stopping rule inside the native loop: the reference exit iteration and iterate, even
     though the overlapped schedule launches the next iteration before the stop decision."""
