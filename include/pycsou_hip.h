@@ -238,7 +238,16 @@ typedef struct {
                              partials, then add pre_partials, into sums_out[4] (no loop control) */
   const double* pre_partials; /* [n_pre][4] partials of an earlier launch of the same iteration */
   int64_t n_pre;
+  /* optional, fkind PCS_F_SEPCONV (fp32, half <= 7): grad F = N x - cty with N = Conv^T Conv
+   * applied as two (4 tier + 1)-tap passes (the normal-operator row-marching kernel).  cty: Conv^T y
+   * in y's layout (halo_y rows); ntaps: pcs_pds2d_ntaps_len(half) fp32 values, the window taps of
+   * N along axis 0 and axis 1 and their exact rows on the tier rows / columns nearest each image
+   * edge (layout in pds_nmarch.hpp; pycsou_amd.opt.engine.nmarch_taps builds it).  NULL: grad F
+   * = Conv^T (Conv x - y) as four (2 tier + 1)-tap passes. */
+  const void* cty;
+  const void* ntaps;
 } pcs_pds2d_args;
+int pcs_pds2d_ntaps_len(int half); /* 64 + 32 * tier(half); -1 beyond tier 7 */
 
 int pcs_pds2d_halo_x(int half);
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);

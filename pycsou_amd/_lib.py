@@ -38,7 +38,8 @@ class PdsArgs(ctypes.Structure):
                 ('step0', _c_dbl), ('step1', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp),
-                ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64)]
+                ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64),
+                ('cty', _vp), ('ntaps', _vp)]
 
 
 class StencilArgs(ctypes.Structure):
@@ -118,6 +119,7 @@ _SIGS = {
     'pcs_apgd_step': (_c_int, [_c_int, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_dbl, _c_dbl, _c_int, _c_dbl, _c_dbl,
                                 _c_dbl, _vp, _vp, _vp]),
     'pcs_pds2d_halo_x': (_c_int, [_c_int]),
+    'pcs_pds2d_ntaps_len': (_c_int, [_c_int]),
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),

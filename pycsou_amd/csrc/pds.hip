@@ -9,6 +9,7 @@
 // precomputed gradient buffer; K = Gradient(kind='forward'); H = lam*L1 / lam*L21 (pixel
 // groups); G = Null / NonNegativeOrthant / Segment.  The tile kernel is in pds_tile.hpp.
 #include "pds_march.hpp"
+#include "pds_nmarch.hpp"
 #include "pds_pt.hpp"
 
 namespace pcs {
@@ -203,11 +204,41 @@ static int march_slots() {
 // One march task = one 64-column strip x one row segment; as many segments as fill the
 // device in one wave of resident workgroups.  False for narrow images (the tile kernel).
 template <int H>
+static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p);
+
+// the normal-operator march kernel (pds_nmarch.hpp): fp32 separable tiers 3 / 7 with the host's
+// Conv^T y and N tables; images of at least 64 x 64 (the edge bands of N never overlap)
+static bool use_nmarch(const pcs_pds2d_args* a) {
+  return a->cty != nullptr && a->ntaps != nullptr && aligned16(a->cty) && a->n0 >= 64 && a->n1 >= 64;
+}
+
+template <int H>
+static int nmarch_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kMarchNT>, kMarchNT,
+                                                     0) != hipSuccess ||
+        nb < 1)
+      nb = 3;
+    (void)hipGetLastError();
+    slots = cus * nb;
+    const char* e = getenv("PCS_NMARCH_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
+  }
+  return slots;
+}
+
+template <int H>
 static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
-  using M = March<H>;
-  const int tiles_x = (int)((a->n1 + M::TW - 1) / M::TW);
+  const bool nm = use_nmarch(a);
+  const int tw = nm ? NMarch<H>::TO : March<H>::TW;
+  const int tiles_x = (int)((a->n1 + tw - 1) / tw);
   if (tiles_x < 2) return false;
-  plan_bands(rb, M::TS, tiles_x, march_slots<H>(), 1, p);
+  plan_bands(rb, March<H>::TS, tiles_x, nm ? nmarch_slots<H>() : march_slots<H>(), 1, p);
   return true;
 }
 
@@ -234,6 +265,13 @@ static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
+  if (use_nmarch(a)) {
+    k_pds2d_nmarch<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
+        (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->cty,
+        (const float*)a->ntaps, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x,
+        p.bd, p.ntasks);
+    return launch_status();
+  }
   k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
@@ -407,6 +445,11 @@ using namespace pcs;
 extern "C" {
 
 int pcs_pds2d_halo_x(int half) { return 1 + 2 * tier_for(half < 0 ? 0 : half); }
+
+int pcs_pds2d_ntaps_len(int half) {
+  const int t = tier_for(half < 0 ? 0 : half);
+  return (t == 3 || t == 7) ? 64 + 32 * t : -1;
+}
 
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
   if (!a || a->rows < 1 || a->n1 < 1) return -1;

@@ -99,6 +99,9 @@ __device__ __forceinline__ void band_rows(const Bands& bd, int seg, int& s0, int
   }
 }
 
+#ifndef PCS_ABL
+#define PCS_ABL 0
+#endif
 // 32-bit slab geometry (the host checks (rows + 2 halo) * n1 < 2^31 for this kernel)
 struct Slab32 {
   int n0, n1, row0, rows, hx, hy, hz, vec;
@@ -126,7 +129,28 @@ template <int AUX = 0>
 __device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, const G4<float>& g) {
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
   const u4 d = {__float_as_uint(g.v[0]), __float_as_uint(g.v[1]), __float_as_uint(g.v[2]), __float_as_uint(g.v[3])};
+#if PCS_ABL & 1024
+  if (PCS_ABL) off = kOOB;
+#endif
   __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)off, 0, AUX);
+}
+
+// Diagnostic ablation builds only (-DPCS_ABL=bits, tools/build_var.sh): 1 = z not landed in LDS,
+// 2 = y not parked, 4 = new x rows not stored, 8/16/32 = P1/P2/P3 skipped, 64/128 = P45/P6 reduced to
+// their stores, 256 = without those stores, 512 = no LDS barriers, 1024 = loads from 4 rows (L2-resident) and
+// stores dropped: compute with almost no HBM traffic (results wrong; timing only).
+// z of step k+1 is loaded at the top of step k and landed in LDS at the top of step k+1, so its
+// latency hides behind a whole step (0: loaded and landed within the step, behind P1-P3 only)
+#ifndef PCS_ZAHEAD
+#define PCS_ZAHEAD 1
+#endif
+#if PCS_ABL & 512
+#define PCS_MB() do { } while (0)
+#else
+#define PCS_MB() lds_barrier()
+#endif
+__device__ __forceinline__ void keep4(const G4<float>& g) {
+  asm volatile("" ::"v"(g.v[0]), "v"(g.v[1]), "v"(g.v[2]), "v"(g.v[3]));
 }
 
 // One halo'd array: its descriptor, row pitch in bytes, and the local rows it can supply
@@ -136,6 +160,9 @@ struct View {
   int halo, lo, hi;
   uint32_t pitch;
   __device__ __forceinline__ uint32_t row_off(int lr) const {
+#if PCS_ABL & 1024
+    if (PCS_ABL) return ((unsigned)(lr - lo) <= (unsigned)(hi - lo)) ? (uint32_t)((lr & 3) + halo) * pitch : kOOB;
+#endif
     return ((unsigned)(lr - lo) <= (unsigned)(hi - lo)) ? (uint32_t)(lr + halo) * pitch : kOOB;
   }
 };
@@ -299,6 +326,12 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   };
   auto store_y = [&](const G4<T>(&yv)[NG2], int cs) {  // parked where P2 writes r
     T* dst = RR + ((cs + p2_r - rb) & 31) * WR;
+#if PCS_ABL & 2
+    if (PCS_ABL) {
+      for (int q = 0; q < NG2; ++q) keep4(yv[q]);
+      return;
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < NG2; ++q)
       if (GR % NG2 == 0 || p2_g0 + q < GR) st4(dst + 4 * (p2_g0 + q), yv[q]);
@@ -308,6 +341,12 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
     for (int k = 0; k < KXN; ++k) xv[k] = bload4(vx.r, vx.row_off(r0 + rr_xn[k]) + co_xn[k]);
   };
   auto store_xn = [&](const G4<T>(&xv)[KXN], int r0) {
+#if PCS_ABL & 4
+    if (PCS_ABL) {
+      for (int k = 0; k < KXN; ++k) keep4(xv[k]);
+      return;
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < KXN; ++k) {
       if (!PCS_WAVE_ON(k, M::NXN)) continue;
@@ -324,6 +363,13 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
     for (int k = 0; k < KZ1; ++k) zr1[k] = bload4(vz1.r, vz1.row_off(a + rr_z1[k]) + co_z1[k]);
   };
   auto land_z = [&](const G4<T>(&zr0)[KZ0], const G4<T>(&zr1)[KZ1]) {
+#if PCS_ABL & 1
+    if (PCS_ABL) {
+      for (int k = 0; k < KZ0; ++k) keep4(zr0[k]);
+      for (int k = 0; k < KZ1; ++k) keep4(zr1[k]);
+      return;
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < KZ0; ++k)
       if (PCS_WAVE_ON(k, M::NZ0)) st4(Z0 + 4 * PCS_ITEM(k, M::NZ0), zr0[k]);
@@ -333,6 +379,9 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   };
   // ---- P1: A rows [cs, cs + TS) = column conv of x (forward: out[i] = sum_t w0[2H - t] x[i - H + t])
   auto p1 = [&](int cs) {
+#if PCS_ABL & 8
+    if (PCS_ABL) return;
+#endif
     const int sl = (cs + 2 * hb - H - xb) & 31;
     T w0[NT2];
     ldtaps(0, w0);
@@ -343,6 +392,9 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   };
   // ---- P2: residual rows [cs, cs + TS) = row conv of A - y (y parked in RR), 0 outside the image
   auto p2 = [&](int cs, int fl) {
+#if PCS_ABL & 16
+    if (PCS_ABL) return;
+#endif
     constexpr int NV = NG2 + H4 / 2;
     T w1[NT2];
     ldtaps(1, w1);
@@ -377,6 +429,9 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   };
   // ---- P3: B rows [a + 1, a + 1 + TS) = column correlation of r (out[i] = sum_t w0[t] r[i - H + t])
   auto p3 = [&](int a) {
+#if PCS_ABL & 32
+    if (PCS_ABL) return;
+#endif
     const int sl = (a + 1 + 2 * hb - H - rb) & 31;
     T w0[NT2];
     ldtaps(0, w0);
@@ -389,6 +444,16 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   //      u = 2 x_t - x on columns [c, c + 5) (column c + 4 = the next group's first: only group 15
   //      stores it, for P6's right neighbour), x' = rho x_t + (1 - rho) x
   auto p45 = [&](int a, int fl, int ub) {
+#if PCS_ABL & 64
+    if (PCS_ABL) {
+      const int lr = a + 1 + ui;
+      const G4<T> xv4 = lds4(XR + ((lr - xb) & 31) * WX + 2 * H4 + 4 * ug);
+      const bool own = lr >= s0 && lr < s1 && s.row0 + lr < s.n0 && ((fl >> 2) & 1);
+      if (PCS_ABL & 256) keep4(xv4);
+      else bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xv4);
+      return;
+    }
+#endif
     const int i = ui, g = ug;
     const int lr = a + 1 + i, gr = s.row0 + lr;
     int slot = i + 1 + ub;
@@ -454,6 +519,21 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
   };
   // ---- P6: z' on row lr = a + ui
   auto p6 = [&](int a, int fl, int ub) {
+#if PCS_ABL & 128
+    if (PCS_ABL) {
+      const int lr = a + ui;
+      const G4<T> zv0 = lds4(Z0 + ui * WG + 4 * ug);
+      const bool own = lr < s1 && s.row0 + lr < s.n0 && ((fl >> 2) & 1);
+      const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_u;
+      if (PCS_ABL & 256) {
+        keep4(zv0);
+      } else {
+        bstore4(rzn0, off, zv0);
+        bstore4(rzn1, off, zv0);
+      }
+      return;
+    }
+#endif
     const int i = ui, g = ug;
     const int lr = a + i, gr = s.row0 + lr;
     int sl0 = i + ub, sl1 = i + 1 + ub;
@@ -524,17 +604,18 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
     load_y(ynx, rb + TS);  // chunk 0's y
     load_z(zr0, zr1, s0 - TS);
   }
-  lds_barrier();
+  PCS_MB();
   p1(rb);
-  lds_barrier();
+  PCS_MB();
   store_y(ynx, rb + TS);
   p2(rb, launder(flags));
-  lds_barrier();
+  PCS_MB();
   p3(s0 - TS);  // B row TS - 1 = row s0 (the rows above it read stale ring rows: unused)
   land_z(zr0, zr1);
-  lds_barrier();
+  if (PCS_ZAHEAD) load_z(zr0, zr1, s0);  // step 0's z (landed at the top of step 0)
+  PCS_MB();
   p45(s0 - TS, launder(flags), 1);  // u on row s0 -> ring slot 0, x' on row s0 (other rows: not own)
-  lds_barrier();
+  PCS_MB();
   store_xn(xnx, s0 + 2 * H + 1);
 
   // ================= march: step k covers B / u / x' rows [a + 1, a + TS], z' rows [a, a + TS)
@@ -547,32 +628,33 @@ __device__ __forceinline__ void march_task(const T* __restrict__ x, T* __restric
     const int a = s0 + k * TS;
     const int cs = a + H + 1;  // residual chunk k rows [cs, cs + TS)
     PCS_ST(0);
-    lds_barrier();  // step k-1 done with U, Z, B and with the XR rows landed in its P6
+    PCS_MB();  // step k-1 done with U, Z, B and with the XR rows landed in its P6
     PCS_ST(1);
     const int fl = launder(flags);
-    // ---- this step's global loads, all issued here (first use: after P3 / in P6)
+    // ---- this step's global loads, all issued here (first use: after P3 / in P6, or next step)
+    if (PCS_ZAHEAD) land_z(zr0, zr1);  // z of this step, loaded during the previous one
     load_xn(xnx, a + TS + 2 * H + 1);  // chunk k+1's new x rows
     load_y(ynx, cs + TS);              // chunk k+1's y
-    load_z(zr0, zr1, a);
+    load_z(zr0, zr1, PCS_ZAHEAD ? a + TS : a);
     PCS_ST(2);
     p1(cs);
     PCS_ST(3);
-    lds_barrier();
+    PCS_MB();
     PCS_ST(4);
     p2(cs, fl);
     PCS_ST(5);
-    lds_barrier();
+    PCS_MB();
     PCS_ST(6);
     p3(a);
     PCS_ST(7);
-    land_z(zr0, zr1);
+    if (!PCS_ZAHEAD) land_z(zr0, zr1);
     PCS_ST(8);
-    lds_barrier();
+    PCS_MB();
     PCS_ST(9);
     store_y(ynx, cs + TS);  // RR slots of chunk k+1 held chunk k-1, last read by P3 above
     p45(a, fl, ub);
     PCS_ST(10);
-    lds_barrier();
+    PCS_MB();
     PCS_ST(11);
     p6(a, fl, ub);
     store_xn(xnx, a + TS + 2 * H + 1);  // XR slots of rows P45 read above

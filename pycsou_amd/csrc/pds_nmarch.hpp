@@ -1,0 +1,459 @@
+// Row-marching fused 2-D PDS iteration through the NORMAL operator of the separable blur
+// (fp32, tiers H = 3 / 7): grad F = Conv^T (Conv x - y) = N x - b with
+//   N = Conv^T Conv = N_v (x) N_h        (the column and row passes commute, so N factors)
+//   b = Conv^T y                          (formed once per problem by the host: pcs_pds2d_args.cty)
+// so an iteration applies two (4H+1)-tap passes instead of four (2H+1)-tap passes, with no
+// residual ring and one LDS round trip per pass.  Away from the image edges N_v / N_h are the
+// autocorrelation of the taps; on the H rows (columns) nearest an edge the zero-boundary
+// truncation between Conv and Conv^T changes the window taps -- the host tables
+// (pcs_pds2d_args.ntaps, below) hold the exact rows of N there.  Same update as the 4-pass
+// march kernel (pds_march.hpp); the iterates differ from it only by fp32 rounding.
+//
+// One workgroup (256 threads) owns TO = 60 columns of a row segment [s0, s1) and computes
+// TW = 64 (the 61st column's u is what K u of the 60th needs), marching 16 rows per step:
+//   top   land z of this step (loaded during the previous one); issue the next step's loads:
+//         x rows [a+2H+17, a+2H+33), b rows [a+17, a+33), z rows [a+16, a+33)
+//   PH    t = N_h x on rows [a+2H+1, a+2H+17)           x ring (32 rows) -> t ring (64 rows)
+//   PV    g = N_v t - b on rows [a+1, a+17); x_t = prox_G(x - tau g - tau K^T z),
+//         u = 2 x_t - x -> u ring, x' = rho x_t + (1 - rho) x
+//   P6    z' = rho fenchel(z + sigma K u) + (1 - rho) z on rows [a, a+16)
+//         park the next step's x rows in the x ring
+// Three barriers per step (the 4-pass kernel has five).
+//
+// ntaps (fp32, 64 + 32 H values): [0, 32) N_v window taps tv[q] (q = 0..4H: row r - 2H + q) =
+// the autocorrelation of the axis-0 taps, [32, 64) the same along axis 1, then the truncation
+// corrections E (H x 8 each, N = window - E on the edge band): E_v for rows 0..H-1 against rows
+// 0..H-1, E_v for rows n0-H+j against rows n0-H+k, E_h for columns 0..H-1, E_h for the last H.
+// Reference: PrimalDualSplitting.update_iterand, pycsou/opt/proxalgs.py:343-355, with
+// grad F = Conv^T((2 (Conv x - y)) 0.5) (core/map.py:609-610), Conv from
+// pycsou/linop/conv.py:167-295.
+#pragma once
+// waves per SIMD the register budget targets (diagnostics builds override)
+#ifndef PCS_NM_WPE
+#define PCS_NM_WPE 3
+#endif
+// window rows per PV read chunk (2 chunks in flight)
+#ifndef PCS_NM_PF
+#define PCS_NM_PF 2
+#endif
+#ifndef PCS_NM_SB
+#define PCS_NM_SB 1
+#endif
+#ifndef PCS_NM_EDGE
+#define PCS_NM_EDGE 1
+#endif
+
+#include "pds_march.hpp"
+
+namespace pcs {
+
+// compiler-only fence: no memory access (LDS reads included) moves across it, at IR or MIR level
+// (bounds the reads in flight, hence the registers they occupy); emits no instruction
+__device__ __forceinline__ void pcs_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// the value is live (computed) at this point: arithmetic is not sunk past it
+__device__ __forceinline__ void pin4(G4<float>& g) {
+  asm volatile("" : "+v"(g.v[0]), "+v"(g.v[1]), "+v"(g.v[2]), "+v"(g.v[3]));
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int H>
+struct NMarch {
+  static constexpr int TW = 64, TO = 60, TS = 16, NQ = 4 * H + 1;
+  static constexpr int XL = RU4<2 * H>::value, SHX = XL - 2 * H;  // x region [c0 - XL, c0 + TW + XL)
+  static constexpr int GXL = (TW + 2 * XL) / 4;                    // loaded x groups per row (24 / 20)
+  static constexpr int WX = TW + 2 * XL + 4;                       // x ring pitch (odd slot count)
+  static constexpr int XRING = 32, TRING = 64;
+  static constexpr int WT = TW, WU = TW + 4;  // t rows: 256 B (ring = 16 KB)
+  // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 16 groups, z1 rows
+  // of 17 groups (from column c0 - 4); 5 wave-instructions of 64 x 16 B each
+  static constexpr int WZ0 = TW, WZ1 = TW + 4, ZSLOTS = 5 * 64;
+  static constexpr int NVH = (SHX + 3 + 4 * H) / 4 + 1;  // b128 groups a PH item reads
+  static constexpr int NXN = TS * GXL;                   // x items per step
+  static constexpr int NXP = (4 * H + 1) * GXL;          // prologue x items
+  static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + TRING * WT, O_W = O_U + (TS + 1) * WU,
+                       NW = 64 + 32 * H, SZ = O_W + NW;  // W: the ntaps table
+  static_assert((TS + 1) * (TW / 4) <= ZSLOTS && (TS + 1) * (TW / 4 + 1) <= ZSLOTS, "z tiles");
+  static_assert(H == 3 || H == 7, "tiers 3 and 7");
+  static_assert(TS + 2 * H + 1 + TS <= XRING + 1 + 2 * H, "x ring holds rows [a+1, a+2H+17)");
+  static_assert(2 * (2 * H) + TS <= TRING - TS, "t ring: the rows PH writes never hold a row PV reads");
+  static_assert(4 * (NVH - 1) + 3 >= SHX + 3 + 4 * H, "PH window");
+  static_assert((WX / 4) % 2 == 1, "odd x slot pitch");
+};
+
+template <typename T, int H, int HK, int NT>
+__device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z,
+                                            T* __restrict__ zn, const T* __restrict__ b,
+                                            const T* __restrict__ tq, const Slab32& s, const Params<T>& P, int gk,
+                                            int s0, int s1, int c0, T* sm, T* Z0, T* Z1, double (&part)[4]) {
+  static_assert(sizeof(T) == 4 && NT == 256, "fp32, 256 threads (4 rows x 16 column groups per wave)");
+  using M = NMarch<H>;
+  constexpr int TS = M::TS, TW = M::TW, TO = M::TO, NQ = M::NQ, XL = M::XL, SHX = M::SHX, NVH = M::NVH;
+  constexpr int WX = M::WX, WT = M::WT, WU = M::WU, WZ0 = M::WZ0, WZ1 = M::WZ1, GXL = M::GXL;
+  constexpr int KXN = cdiv(M::NXN, NT), KXP = cdiv(M::NXP, NT);
+  constexpr int GG = TW / 4;
+  T* XR = sm + M::O_XR;
+  T* TR = sm + M::O_T;
+  T* U = sm + M::O_U;
+  T* W = sm + M::O_W;  // taps (broadcast reads, re-read per phase: none live across the loop)
+  const T* Wq = W;     // the taps' address, laundered every step (no loop-invariant tap reads)
+  for (int i = threadIdx.x; i < M::NW; i += NT) W[i] = tq[i];  // visible after the first barrier
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hb = tid >> 5, l5 = tid & 31;
+  const int ui = 2 * hb + lane_grp(l5), ug = lane_idx(l5);  // every phase: row ui, column group ug
+  const int n0 = s.n0, n1 = s.n1;
+  const int zstride = (s.rows + 2 * s.hz) * n1;
+  const int xc0 = c0 - XL;
+  const View vx = make_view(x, s, s.hx), vb = make_view(b, s, s.hy), vz0 = make_view(z, s, s.hz),
+             vz1 = make_view(z + zstride, s, s.hz);
+  const uint32_t pitch = (uint32_t)n1 * 4u;
+  const Rsrc rxn = rsrc_of(xn, (uint32_t)(s.rows + 2 * s.hx) * pitch);
+  const Rsrc rzn0 = rsrc_of(zn, (uint32_t)zstride * 4u), rzn1 = rsrc_of(zn + zstride, (uint32_t)zstride * 4u);
+#define PCS_WAVE_ON(k, N) ((k) * NT + wv * 64 < (N))
+#define PCS_ITEM(k, N) min((k) * NT + tid, (N) - 1)
+
+  // ---- per-thread geometry
+  const int ucg = c0 + 4 * ug;
+  const uint32_t co_u = col_off(ucg, n1);
+  const bool cin = ucg < n1;                        // group in the image (4-groups wholly in / out)
+  const bool clast = ucg == n1 - 4;                 // holds the image's last column
+  const bool cown = ug < TO / 4 && cin;             // stored by this workgroup
+  uint32_t co_xn[KXN];
+  int rr_xn[KXN];
+#pragma unroll
+  for (int k = 0; k < KXN; ++k) {
+    const int e = PCS_ITEM(k, M::NXN);
+    rr_xn[k] = e / GXL;
+    co_xn[k] = col_off(xc0 + 4 * (e - (e / GXL) * GXL), n1);
+  }
+
+  auto load_xn = [&](G4<T>(&xv)[KXN], int r0) {  // x rows [r0, r0 + TS) of the x region
+#pragma unroll
+    for (int k = 0; k < KXN; ++k) xv[k] = bload4(vx.r, vx.row_off(r0 + rr_xn[k]) + co_xn[k]);
+  };
+  auto store_xn = [&](const G4<T>(&xv)[KXN], int r0) {
+#pragma unroll
+    for (int k = 0; k < KXN; ++k) {
+      if (!PCS_WAVE_ON(k, M::NXN)) continue;
+      const int e = PCS_ITEM(k, M::NXN);
+      const int r = e / GXL, g = e - (e / GXL) * GXL;
+      st4(XR + ((r0 + r) & 31) * WX + 4 * g, xv[k]);
+    }
+  };
+  // z0 rows [a, a + TS], cols [c0, c0 + TW) -> Z0; z1 rows [a, a + TS], cols [c0 - 4, c0 + TW) -> Z1,
+  // straight into LDS (buffer_load ... lds: no VGPRs, no ds_write).  Wave w issues tile
+  // instructions w and w + 4 of each tile: lane l of instruction j fills slot 64 j + l (rows past
+  // the tile and rows below `rmin` read as 0).  The issuing waves wait for them (vmcnt) before the
+  // barrier that precedes the first read.
+  const int lane = tid & 63;
+  auto load_z = [&](int a, int rmin) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = wv + 4 * jj;
+      if (j < 5) {
+        const int e = 64 * j + lane;
+        const int r0 = e >> 4, g0 = e & 15;  // z0: 16 groups per row
+        const int r1 = e / 17, g1 = e - 17 * (e / 17);  // z1: 17 groups per row
+        const uint32_t o0 = (r0 > TS || r0 < rmin ? kOOB : vz0.row_off(a + r0)) + col_off(c0 + 4 * g0, n1);
+        const uint32_t o1 = (r1 > TS || r1 < rmin ? kOOB : vz1.row_off(a + r1)) + col_off(c0 - 4 + 4 * g1, n1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vz0.r, (__attribute__((address_space(3))) void*)(Z0 + 256 * j), 16,
+                                                 o0, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vz1.r, (__attribute__((address_space(3))) void*)(Z1 + 256 * j), 16,
+                                                 o1, 0, 0, 0);
+      }
+    }
+  };
+  // ---- PH: t row lr = N_h x row lr on columns [c0 + 4 ug, + 4) -> t ring
+  auto ph = [&](int lr) {
+    const T* xrow = XR + (lr & 31) * WX;
+    T v[4 * NVH];
+#pragma unroll
+    for (int q = 0; q < NVH; ++q) {
+      const G4<T> t4 = lds4(xrow + 4 * ug + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = t4.v[e];
+    }
+    G4<T> o;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o.v[m] = T(0);
+#pragma unroll
+    for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {  // taps 4 at a time (broadcast LDS reads)
+      const G4<T> w4 = lds4(Wq + 32 + 4 * q4);
+      if (PCS_NM_SB) pcs_fence();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 4 * q4 + e;
+        if (q < NQ) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) o.v[m] += w4.v[e] * v[SHX + m + q];
+        }
+      }
+      pin4(o);
+    }
+    pcs_fence();
+    if (PCS_NM_EDGE && c0 < H) {  // exact rows of N_h on the H columns nearest the left image edge
+      const G4<T> x0 = lds4(xrow + XL), x1 = lds4(xrow + XL + 4);  // image columns 0..7
+      const T xe[8] = {x0.v[0], x0.v[1], x0.v[2], x0.v[3], x1.v[0], x1.v[1], x1.v[2], x1.v[3]};
+      const bool on = ug < 2;
+      const T* et = Wq + 64 + 16 * H + 4 * (on ? ug : 0);
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const G4<T> e4 = lds4(et + 8 * k);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o.v[m] -= (on ? e4.v[m] : T(0)) * xe[k];
+      }
+    }
+    if (PCS_NM_EDGE && c0 + TW > n1 - H) {  // ... and the right one (image columns n1 - 8 .. n1 - 1)
+      const T* xr8 = xrow + (n1 - 8 - xc0);
+      const G4<T> x0 = lds4(xr8), x1 = lds4(xr8 + 4);
+      const T xf[8] = {x0.v[0], x0.v[1], x0.v[2], x0.v[3], x1.v[0], x1.v[1], x1.v[2], x1.v[3]};
+      const int j = ucg - (n1 - 8);
+      const bool on = j == 0 || j == 4;
+      const T* et = Wq + 64 + 24 * H + (on ? j : 0);
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const G4<T> e4 = lds4(et + 8 * k);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o.v[m] -= (on ? e4.v[m] : T(0)) * xf[8 - H + k];
+      }
+    }
+    st4(TR + (lr & 63) * WT + 4 * ug, o);
+  };
+  // ---- PV + update: row lr = a + 1 + ui
+  auto pv = [&](int a, const G4<T>& bv, int ub) {
+    const int lr = a + 1 + ui, gr = s.row0 + lr;
+    int slot = ui + 1 + ub;
+    slot = slot >= 17 ? slot - 17 : slot;
+    // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring.  The ring is 64 rows of 256 B, so the
+    // byte address of window row q is ((row bytes + 256 q) & 16383) | column bytes (2 VALU per
+    // read); reads are issued in chunks of PF behind a scheduling fence (at most 2 PF in flight)
+    G4<T> g;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) g.v[m] = T(0);
+    const uint32_t rb0 = (uint32_t)((lr - 2 * H) & 63) * (WT * 4), cb = (uint32_t)ug * 16u;
+    const char* tbase = reinterpret_cast<const char*>(TR);
+    constexpr int PF = PCS_NM_PF, NCH = (NQ + PF - 1) / PF;  // window rows per chunk
+    G4<T> buf[2][PF];
+    auto rd = [&](int q) {
+      return lds4(reinterpret_cast<const T*>(tbase + (((rb0 + 256u * q) & 16383u) | cb)));
+    };
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (j < NQ) buf[0][j] = rd(j);
+    G4<T> w4;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j)
+          if ((c + 1) * PF + j < NQ) buf[(c + 1) & 1][j] = rd((c + 1) * PF + j);
+      }
+      if ((c * PF) % 4 == 0) w4 = lds4(Wq + c * PF);  // the next 4 taps
+      pcs_fence();
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        if (c * PF + j < NQ) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) g.v[m] += w4.v[(c * PF + j) & 3] * buf[c & 1][j].v[m];
+        }
+      }
+      pin4(g);  // the chunk's FMAs stay here (not sunk below the later reads)
+      pcs_fence();
+    }
+    const int wrow0 = s.row0 + a + 1 + 4 * wv;  // the wave's first global row
+    if (PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H)) {  // the exact rows of N_v on the H rows nearest an image edge
+      const bool top = gr >= 0 && gr < H, bot = gr >= n0 - H && gr < n0;
+      const T* d = Wq + 64 + (top ? 8 * gr : 8 * H + 8 * (gr - (n0 - H)));
+      const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const G4<T> t4 = lds4(TR + ((kr0 + k) & 63) * WT + 4 * ug);
+        const T w = (top || bot) ? d[k] : T(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) g.v[m] -= w * t4.v[m];
+      }
+    }
+    const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
+    const G4<T> za = lds4(Z0 + ui * WZ0 + 4 * ug);               // z0[lr - 1]
+    const G4<T> zb = lds4(Z0 + (ui + 1) * WZ0 + 4 * ug);         // z0[lr]
+    const G4<T> z1a = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug);        // z1[lr][c - 4 .. c - 1]
+    const G4<T> z1b = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug + 4);    // z1[lr][c .. c + 3]
+    const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
+    const bool rrow = gr < n0 && lr <= s.rows;
+    const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+    G4<T> uo, xo;
+    T sdx = T(0), sx = T(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const T gd = g.v[m] - bv.v[m];
+      const T xv = xv4.v[m];
+      // K^T z for forward differences, VStack order: (0 + D0^T z0) + D1^T z1
+      const T zl = (m == 0) ? z1a.v[3] : z1b.v[m - 1];
+      const T zr = z1b.v[m];
+      T d0 = r_first ? T(0) : za.v[m];
+      if (!r_last) d0 -= zb.v[m];
+      const T d1 = zl - ((m == 3 && clast) ? T(0) : zr);
+      const T xt = prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
+      uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
+      const T xnew = P.rho * xt + P.omr * xv;
+      xo.v[m] = xnew;
+      const T dx = xv - xnew;
+      sdx += dx * dx;
+      sx += xv * xv;
+    }
+    if (own) {
+      part[0] += (double)sdx;
+      part[1] += (double)sx;
+    }
+    st4(U + slot * WU + 4 * ug, uo);
+    bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+  };
+  // ---- P6: z' on row lr = a + ui
+  auto p6 = [&](int a, int ub) {
+    const int lr = a + ui, gr = s.row0 + lr;
+    int sl0 = ui + ub, sl1 = ui + 1 + ub;
+    sl0 = sl0 >= 17 ? sl0 - 17 : sl0;
+    sl1 = sl1 >= 17 ? sl1 - 17 : sl1;
+    const G4<T> uc = lds4(U + sl0 * WU + 4 * ug);
+    const G4<T> ud = lds4(U + sl1 * WU + 4 * ug);
+    const G4<T> zv0 = lds4(Z0 + ui * WZ0 + 4 * ug);
+    const G4<T> zv1 = lds4(Z1 + ui * WZ1 + 4 * ug + 4);
+    const T une = U[sl0 * WU + 4 * ug + 4];
+    const bool r_last = gr >= n0 - 1;
+    const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+    G4<T> o0, o1;
+    T sdz = T(0), sz = T(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const T uright = (m < 3) ? uc.v[m + 1] : une;
+      const T d0 = r_last ? T(0) : (ud.v[m] - uc.v[m]);
+      const T d1 = (m == 3 && clast) ? T(0) : (uright - uc.v[m]);
+      const T w0v = zv0.v[m] + P.sigma * (d0 * P.inv_step0), w1v = zv1.v[m] + P.sigma * (d1 * P.inv_step1);
+      const T v0 = w0v * P.inv_sigma, v1 = w1v * P.inv_sigma;
+      T zt0, zt1;
+      if (HK == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
+        T f = T(1) - P.t_h * fast_rsqrt(v0 * v0 + v1 * v1);
+        f = f > T(0) ? f : T(0);
+        zt0 = w0v - P.sigma * (f * v0);
+        zt1 = w1v - P.sigma * (f * v1);
+      } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
+        zt0 = w0v - P.sigma * (v0 - P.t_h * clip1(v0 * P.inv_t_h));
+        zt1 = w1v - P.sigma * (v1 - P.t_h * clip1(v1 * P.inv_t_h));
+      }
+      o0.v[m] = P.rho * zt0 + P.omr * zv0.v[m];
+      o1.v[m] = P.rho * zt1 + P.omr * zv1.v[m];
+      const T e0 = zv0.v[m] - o0.v[m], e1 = zv1.v[m] - o1.v[m];
+      sdz += e0 * e0 + e1 * e1;
+      sz += zv0.v[m] * zv0.v[m] + zv1.v[m] * zv1.v[m];
+    }
+    if (own) {
+      part[2] += (double)sdz;
+      part[3] += (double)sz;
+    }
+    const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_u;
+    bstore4(rzn0, off, o0);
+    bstore4(rzn1, off, o1);
+  };
+
+  // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0
+  G4<T> xnx[KXN], bv;
+  {
+    G4<T> xv[KXP];
+#pragma unroll
+    for (int k = 0; k < KXP; ++k) {
+      const int e = PCS_ITEM(k, M::NXP);
+      const int r = e / GXL, g = e - (e / GXL) * GXL;
+      xv[k] = bload4(vx.r, vx.row_off(s0 - 2 * H + r) + col_off(xc0 + 4 * g, n1));
+    }
+    load_z(s0 - TS, TS - 1);  // z rows s0 - 1, s0 only (the prologue's one update row), b on row s0
+    bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
+#pragma unroll
+    for (int k = 0; k < KXP; ++k) {
+      if (!PCS_WAVE_ON(k, M::NXP)) continue;
+      const int e = PCS_ITEM(k, M::NXP);
+      const int r = e / GXL, g = e - (e / GXL) * GXL;
+      st4(XR + ((s0 - 2 * H + r) & 31) * WX + 4 * g, xv[k]);
+    }
+    vm_wait<0>();
+  }
+  lds_barrier();
+  ph(s0 - 2 * H + ui);  // t rows [s0 - 2H, s0 - 2H + 16)
+  if (ui + TS < 4 * H + 1) ph(s0 - 2 * H + TS + ui);  // t rows [s0 - 2H + 16, s0 + 2H]
+  lds_barrier();
+  if (wv == 3) pv(s0 - TS, bv, 1);  // u on row s0 -> u ring slot 0, x' on row s0 (rows above: not own)
+  load_xn(xnx, s0 + 2 * H + 1);     // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
+  lds_barrier();
+  store_xn(xnx, s0 + 2 * H + 1);  // slots of rows [s0 + 2H - 31, s0 + 2H - 15): read by PH above only
+
+  // ================= march: step k covers t rows [a+2H+1, a+2H+17), u / x' rows [a+1, a+17), z' rows [a, a+16)
+  const int nsteps = (s1 - s0 + TS - 1) / TS;
+  int ub = 0;  // (-k) mod 17: row r = a + j sits in u ring slot (j + ub) mod 17
+  for (int k = 0; k < nsteps; ++k) {
+    const int a = s0 + k * TS;
+    lds_barrier();  // step k-1 done with U, Z and the t / x ring rows it read; its x rows landed
+    asm volatile("" : "+v"(Wq));
+    // this step's z tiles (LDS-DMA) and b, the next step's x rows (registers, landed after P6)
+    load_z(a, 0);
+    bv = bload4(vb.r, vb.row_off(a + 1 + ui) + co_u);
+    load_xn(xnx, a + 2 * H + 1 + TS);
+    ph(a + 2 * H + 1 + ui);
+    vm_wait<KXN + 1>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
+    lds_barrier();
+    pv(a, bv, ub);
+    lds_barrier();
+    p6(a, ub);
+    store_xn(xnx, a + 2 * H + 1 + TS);  // x ring slots of rows [a + 2H - 15, a + 2H + 1): read above
+    ub = ub == 0 ? 16 : ub - 1;
+  }
+#undef PCS_WAVE_ON
+#undef PCS_ITEM
+}
+
+// One block per task (60-column strip x row segment); with `hist` the last workgroups also
+// reduce the partials and run the loop control, with `ro.sums` they only reduce.
+template <typename T, int H, int HK, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))) void k_pds2d_nmarch(
+    const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
+    const T* __restrict__ b, const T* __restrict__ tq, Slab32 s, Params<T> P, int gk, double* __restrict__ partials,
+    Ctrl* ctrl, double* hist, void* ws, RedOut ro, int tiles_x, Bands bd, int ntasks) {
+  using M = NMarch<H>;
+  __shared__ __attribute__((aligned(16))) T sm[M::SZ];
+  __shared__ __attribute__((aligned(16))) T zs0[4 * M::ZSLOTS];  // z tiles: own arrays, so the LDS-DMA
+  __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];  // into them never aliases a ring read
+  __shared__ double red[4 * (NT / 64)];
+  __shared__ int flag[2];
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
+
+  int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
+  {
+    const int bb = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int seg = task / tiles_x, strip = task - seg * tiles_x;
+  int s0, s1;
+  band_rows(bd, seg, s0, s1);
+  const int c0 = strip * M::TO;
+
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  if (!stopped) nmarch_task<T, H, HK, NT>(x, xn, z, zn, b, tq, s, P, gk, s0, s1, c0, sm, zs0, zs1, part);
+  block_sum<4>(part, red);
+  if (hist != nullptr || ro.sums != nullptr) {
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
+  } else if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
+  }
+}
+
+}  // namespace pcs

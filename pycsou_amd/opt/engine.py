@@ -73,6 +73,48 @@ def _match_h(H, ncomp, N):
     return None
 
 
+def nmarch_taps(t0, t1, half):
+    """The N = Conv^T Conv tables of the normal-operator march kernel (pds_nmarch.hpp) for a
+    separable PSF with centred taps t0 (axis 0) and t1 (axis 1) of half width `half`, padded to
+    the tier H (3 or 7): (Conv v)[i] = sum_d c[d] v[i - d], c[d] = t[H + d].  Away from the
+    edges N is the autocorrelation a[e] = sum_m c[m] c[m + e] (window taps a[|q - 2H|],
+    q = 0..4H); on the H samples nearest each edge the zero boundary removes the terms of the
+    samples outside the image: N[j, k] = a[j - k] - E[j][k], E[j][k] = sum_{i < 0} c[i - j] c[i - k]
+    (left / top, j, k < H) and the mirror sum over i >= n on the right / bottom.  Computed in fp64,
+    returned as the fp32 layout the kernel reads (64 + 32 H values)."""
+    H = 3 if half <= 3 else 7
+    out = np.zeros(64 + 32 * H)
+
+    def taps(t):
+        w = np.zeros(2 * H + 1)
+        w[H - half:H + half + 1] = np.asarray(t, dtype=np.float64)
+        return lambda d: w[H + d] if -H <= d <= H else 0.0
+
+    def window(c):
+        a = [sum(c(m) * c(m + e) for m in range(-H, H + 1)) for e in range(2 * H + 1)]
+        return [a[abs(q - 2 * H)] for q in range(4 * H + 1)]
+
+    def e_lo(c):  # E[j][k], j, k < H: the rows i = -H..-1 above the image
+        return [[sum(c(i - j) * c(i - k) for i in range(-H, 0)) for k in range(H)] for j in range(H)]
+
+    def e_hi(c):  # the last H samples, j = n-H+jj, k = n-H+kk, rows i = n..n+H-1 (i - j = H + ii - jj)
+        return [[sum(c(H + ii - jj) * c(H + ii - kk) for ii in range(H)) for kk in range(H)] for jj in range(H)]
+
+    c0, c1 = taps(t0), taps(t1)
+    out[0:4 * H + 1] = window(c0)
+    out[32:32 + 4 * H + 1] = window(c1)
+    ev_lo, ev_hi, eh_lo, eh_hi = e_lo(c0), e_hi(c0), e_lo(c1), e_hi(c1)
+    base = 64
+    for j in range(H):  # E_v rows: [j][k]
+        out[base + 8 * j:base + 8 * j + H] = ev_lo[j]
+        out[base + 8 * H + 8 * j:base + 8 * H + 8 * j + H] = ev_hi[j]
+    for k in range(H):  # E_h transposed: ET[k][c] for the left band, ET[k][i] (column n1-8+i) right
+        for cc in range(H):
+            out[base + 16 * H + 8 * k + cc] = eh_lo[cc][k]
+            out[base + 24 * H + 8 * k + (8 - H) + cc] = eh_hi[cc][k]
+    return out.astype(np.float32)
+
+
 def match_stencil2d(F, G, H, K, has_H):
     """Engine spec for the general-stencil fused step (pcs_pds2d_stencil_step): K a 2-D Gradient of
     any kind (pycsou/linop/diff.py:777-882) or a 2-D Laplacian (diff.py:885-957), H = lam * L1 / L21,
@@ -187,6 +229,13 @@ class PDS2DEngine:
                              torch.as_tensor(t1).to(device=dev, dtype=dtype)]
                 a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
                 a.half = half
+                # PCS_NMARCH=0: diagnostics, the four-pass march kernel (grad F = Conv^T (Conv x - y))
+                if dtype == torch.float32 and half <= 7 and os.environ.get('PCS_NMARCH', '1') != '0':
+                    # normal-operator march kernel: grad F = N x - Conv^T y (pds_nmarch.hpp),
+                    # Conv^T y formed once here in fp64
+                    self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+                    self.cty = conv._adj(-O.to_dev(spec['shift'], torch.float64)).to(dtype).contiguous()
+                    a.cty, a.ntaps = self.cty.data_ptr(), self.ntaps.data_ptr()
             else:
                 fk = L.PCS_F_GRADBUF
                 self.conv = conv

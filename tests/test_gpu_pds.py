@@ -231,13 +231,24 @@ def test_pds3d_fused_matches_reference(name, dtype):
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 def test_pds3d_ata_opt_in_matches_reference(monkeypatch, dtype):
     """The opt-in two-pass gradient (PCS_3D_ATA=1: pcs_conv2d_sep_ata_planes + the axis-0 pass
-    against C12^T y) reproduces the reference trajectory like the default three-pass chain."""
+    against C12^T y).  The golden volume's last axis (22) is not a multiple of 4, which the
+    four-pass kernel needs: there the engine keeps the three-pass chain (same trajectory); on a
+    24 x 20 x 24 volume the two-pass gradient runs and matches the oracle."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     monkeypatch.setenv('PCS_3D_ATA', '1')
     c = pds_case('deconv3d_l21_fwd_24_sep15')
     pds = build(c, dtype, engine='fused')
     _check(pds, c, dtype)
+    assert isinstance(pds._engine, PDS3DEngine) and not pds._engine.ata
+    c = _vol_problem(24, dtype, seed=5, niter=20, shape=(24, 20, 24))
+    pds = build(c, dtype, engine='fused')
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    est, _, _ = pds.iterate()
     assert isinstance(pds._engine, PDS3DEngine) and pds._engine.ata
+    x_ref, z_ref, _ = oracle_pds(c)
+    tol = 1e-10 if dtype == np.float64 else 5e-5
+    assert rel(est['primal_variable'], x_ref) < tol
+    assert rel(est['dual_variable'], z_ref) < tol
 
 
 def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None):

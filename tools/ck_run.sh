@@ -1,9 +1,11 @@
+#!/bin/bash
+# Checkpoint: GPU tests, bench line, kernel-trace stats of the bench (dir under gpurun_out/ = $1)
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r2ck1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r2ck1/gpu_tests.txt 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r2ck1/gpu_tests.txt; exit 1; }
-tail -3 gpurun_out/r2ck1/gpu_tests.txt
-timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 > gpurun_out/r2ck1/bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/r2ck1/bench.log; exit 2; }
-tail -1 gpurun_out/r2ck1/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r2ck1/prof -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/r2ck1/prof.log 2>&1 || { echo PROF_FAILED; tail -20 gpurun_out/r2ck1/prof.log; exit 3; }
+mkdir -p gpurun_out/${1:-ck}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${1:-ck}/gpu_tests.txt 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/${1:-ck}/gpu_tests.txt; exit 1; }
+tail -3 gpurun_out/${1:-ck}/gpu_tests.txt
+timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 > gpurun_out/${1:-ck}/bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/${1:-ck}/bench.log; exit 2; }
+tail -1 gpurun_out/${1:-ck}/bench.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${1:-ck}/prof -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/${1:-ck}/prof.log 2>&1 || { echo PROF_FAILED; tail -20 gpurun_out/${1:-ck}/prof.log; exit 3; }
 echo ALL_OK
