@@ -150,6 +150,7 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
 // ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel (pds_march.hpp) on every
 // 64-column strip, reduction + loop control in its last workgroups
 constexpr int kMarchNT = 256;
+constexpr int kNMarchNT = 256;
 
 struct MarchPlan {
   int tiles_x;  // 64-column strips
@@ -220,7 +221,7 @@ static int nmarch_slots() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kMarchNT>, kMarchNT,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kNMarchNT>, kNMarchNT,
                                                      0) != hipSuccess ||
         nb < 1)
       nb = 3;
@@ -235,7 +236,7 @@ static int nmarch_slots() {
 template <int H>
 static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const bool nm = use_nmarch(a);
-  const int tw = nm ? NMarch<H>::TO : March<H>::TW;
+  const int tw = nm ? NMarch<H>::TW : March<H>::TW;
   const int tiles_x = (int)((a->n1 + tw - 1) / tw);
   if (tiles_x < 2) return false;
   plan_bands(rb, March<H>::TS, tiles_x, nm ? nmarch_slots<H>() : march_slots<H>(), 1, p);
@@ -266,7 +267,7 @@ static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
   if (use_nmarch(a)) {
-    k_pds2d_nmarch<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
+    k_pds2d_nmarch<float, H, HK, kNMarchNT><<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>(
         (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->cty,
         (const float*)a->ntaps, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x,
         p.bd, p.ntasks);

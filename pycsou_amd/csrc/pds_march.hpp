@@ -138,7 +138,8 @@ __device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, const G4<float>& g
 // Diagnostic ablation builds only (-DPCS_ABL=bits, tools/build_var.sh): 1 = z not landed in LDS,
 // 2 = y not parked, 4 = new x rows not stored, 8/16/32 = P1/P2/P3 skipped, 64/128 = P45/P6 reduced to
 // their stores, 256 = without those stores, 512 = no LDS barriers, 1024 = loads from 4 rows (L2-resident) and
-// stores dropped: compute with almost no HBM traffic (results wrong; timing only).
+// stores dropped: compute with almost no HBM traffic, 2048 = normal-operator kernel without its two
+// conv passes (results wrong; timing only).
 // z of step k+1 is loaded at the top of step k and landed in LDS at the top of step k+1, so its
 // latency hides behind a whole step (0: loaded and landed within the step, behind P1-P3 only)
 #ifndef PCS_ZAHEAD

@@ -9,8 +9,10 @@
 // (pcs_pds2d_args.ntaps, below) hold the exact rows of N there.  Same update as the 4-pass
 // march kernel (pds_march.hpp); the iterates differ from it only by fp32 rounding.
 //
-// One workgroup (256 threads) owns TO = 60 columns of a row segment [s0, s1) and computes
-// TW = 64 (the 61st column's u is what K u of the 60th needs), marching 16 rows per step:
+// One workgroup (256 threads: 4 rows x 16 column groups per wave) owns a 64-column strip of a row
+// segment [s0, s1) (strips on 256-B boundaries) and marches down it 16 rows per step; each item
+// also computes the column after its 4 (t, g, u): the strip's 65th column, whose u K u of the 64th
+// needs, comes from the last group's fifth column:
 //   top   land z of this step (loaded during the previous one); issue the next step's loads:
 //         x rows [a+2H+17, a+2H+33), b rows [a+17, a+33), z rows [a+16, a+33)
 //   PH    t = N_h x on rows [a+2H+1, a+2H+17)           x ring (32 rows) -> t ring (64 rows)
@@ -36,9 +38,6 @@
 #ifndef PCS_NM_PF
 #define PCS_NM_PF 2
 #endif
-#ifndef PCS_NM_SB
-#define PCS_NM_SB 1
-#endif
 #ifndef PCS_NM_EDGE
 #define PCS_NM_EDGE 1
 #endif
@@ -59,6 +58,14 @@ __device__ __forceinline__ void pin4(G4<float>& g) {
   asm volatile("" : "+v"(g.v[0]), "+v"(g.v[1]), "+v"(g.v[2]), "+v"(g.v[3]));
 }
 
+__device__ __forceinline__ void pin1(float& v) { asm volatile("" : "+v"(v)); }
+
+// one LDS float (a volatile read: never widened or merged with its neighbours)
+__device__ __forceinline__ float lds1(const float* p) {
+  typedef __attribute__((address_space(3))) const volatile float* lds_f1;
+  return *(lds_f1)(p);
+}
+
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima)
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -68,25 +75,25 @@ __device__ __forceinline__ void vm_wait() {
 
 template <int H>
 struct NMarch {
-  static constexpr int TW = 64, TO = 60, TS = 16, NQ = 4 * H + 1;
+  static constexpr int TW = 64, TS = 16, NQ = 4 * H + 1;
   static constexpr int XL = RU4<2 * H>::value, SHX = XL - 2 * H;  // x region [c0 - XL, c0 + TW + XL)
   static constexpr int GXL = (TW + 2 * XL) / 4;                    // loaded x groups per row (24 / 20)
   static constexpr int WX = TW + 2 * XL + 4;                       // x ring pitch (odd slot count)
   static constexpr int XRING = 32, TRING = 64;
-  static constexpr int WT = TW, WU = TW + 4;  // t rows: 256 B (ring = 16 KB)
+  static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B)
   // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 16 groups, z1 rows
   // of 17 groups (from column c0 - 4); 5 wave-instructions of 64 x 16 B each
-  static constexpr int WZ0 = TW, WZ1 = TW + 4, ZSLOTS = 5 * 64;
+  static constexpr int WZ0 = TW + 4, WZ1 = TW + 8, ZSLOTS = 5 * 64;
   static constexpr int NVH = (SHX + 3 + 4 * H) / 4 + 1;  // b128 groups a PH item reads
   static constexpr int NXN = TS * GXL;                   // x items per step
   static constexpr int NXP = (4 * H + 1) * GXL;          // prologue x items
   static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + TRING * WT, O_W = O_U + (TS + 1) * WU,
                        NW = 64 + 32 * H, SZ = O_W + NW;  // W: the ntaps table
-  static_assert((TS + 1) * (TW / 4) <= ZSLOTS && (TS + 1) * (TW / 4 + 1) <= ZSLOTS, "z tiles");
+  static_assert((TS + 1) * (WZ0 / 4) <= ZSLOTS && (TS + 1) * (WZ1 / 4) <= ZSLOTS, "z tiles");
   static_assert(H == 3 || H == 7, "tiers 3 and 7");
   static_assert(TS + 2 * H + 1 + TS <= XRING + 1 + 2 * H, "x ring holds rows [a+1, a+2H+17)");
   static_assert(2 * (2 * H) + TS <= TRING - TS, "t ring: the rows PH writes never hold a row PV reads");
-  static_assert(4 * (NVH - 1) + 3 >= SHX + 3 + 4 * H, "PH window");
+  static_assert(4 * (NVH - 1) + 3 >= SHX + 4 + 4 * H, "PH window (5 outputs)");
   static_assert((WX / 4) % 2 == 1, "odd x slot pitch");
 };
 
@@ -97,7 +104,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
                                             int s0, int s1, int c0, T* sm, T* Z0, T* Z1, double (&part)[4]) {
   static_assert(sizeof(T) == 4 && NT == 256, "fp32, 256 threads (4 rows x 16 column groups per wave)");
   using M = NMarch<H>;
-  constexpr int TS = M::TS, TW = M::TW, TO = M::TO, NQ = M::NQ, XL = M::XL, SHX = M::SHX, NVH = M::NVH;
+  constexpr int TS = M::TS, TW = M::TW, NQ = M::NQ, XL = M::XL, SHX = M::SHX, NVH = M::NVH;
   constexpr int WX = M::WX, WT = M::WT, WU = M::WU, WZ0 = M::WZ0, WZ1 = M::WZ1, GXL = M::GXL;
   constexpr int KXN = cdiv(M::NXN, NT), KXP = cdiv(M::NXP, NT);
   constexpr int GG = TW / 4;
@@ -127,7 +134,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   const uint32_t co_u = col_off(ucg, n1);
   const bool cin = ucg < n1;                        // group in the image (4-groups wholly in / out)
   const bool clast = ucg == n1 - 4;                 // holds the image's last column
-  const bool cown = ug < TO / 4 && cin;             // stored by this workgroup
+  const bool cown = cin;                            // stored by this workgroup
   uint32_t co_xn[KXN];
   int rr_xn[KXN];
 #pragma unroll
@@ -150,9 +157,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       st4(XR + ((r0 + r) & 31) * WX + 4 * g, xv[k]);
     }
   };
-  // z0 rows [a, a + TS], cols [c0, c0 + TW) -> Z0; z1 rows [a, a + TS], cols [c0 - 4, c0 + TW) -> Z1,
+  // z0 rows [a, a + TS], cols [c0, c0 + TW + 4) -> Z0; z1 rows [a, a + TS], cols [c0 - 4, c0 + TW + 4) -> Z1,
   // straight into LDS (buffer_load ... lds: no VGPRs, no ds_write).  Wave w issues tile
-  // instructions w and w + 4 of each tile: lane l of instruction j fills slot 64 j + l (rows past
+  // instructions w and w + 4 of each tile (5 each): lane l of instruction j fills slot 64 j + l (rows past
   // the tile and rows below `rmin` read as 0).  The issuing waves wait for them (vmcnt) before the
   // barrier that precedes the first read.
   const int lane = tid & 63;
@@ -162,8 +169,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const int j = wv + 4 * jj;
       if (j < 5) {
         const int e = 64 * j + lane;
-        const int r0 = e >> 4, g0 = e & 15;  // z0: 16 groups per row
-        const int r1 = e / 17, g1 = e - 17 * (e / 17);  // z1: 17 groups per row
+        const int r0 = e / 17, g0 = e - 17 * (e / 17);  // z0: 17 groups per row (cols c0 .. c0 + 67)
+        const int r1 = e / 18, g1 = e - 18 * (e / 18);  // z1: 18 groups per row (cols c0 - 4 .. c0 + 67)
         const uint32_t o0 = (r0 > TS || r0 < rmin ? kOOB : vz0.row_off(a + r0)) + col_off(c0 + 4 * g0, n1);
         const uint32_t o1 = (r1 > TS || r1 < rmin ? kOOB : vz1.row_off(a + r1)) + col_off(c0 - 4 + 4 * g1, n1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vz0.r, (__attribute__((address_space(3))) void*)(Z0 + 256 * j), 16,
@@ -173,7 +180,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       }
     }
   };
-  // ---- PH: t row lr = N_h x row lr on columns [c0 + 4 ug, + 4) -> t ring
+  // ---- PH: t row lr = N_h x row lr on columns [c0 + 4 ug, + 5) -> t ring (the fifth column is
+  // kept by the last group only: the strip's 65th column)
   auto ph = [&](int lr) {
     const T* xrow = XR + (lr & 31) * WX;
     T v[4 * NVH];
@@ -184,21 +192,24 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       for (int e = 0; e < 4; ++e) v[4 * q + e] = t4.v[e];
     }
     G4<T> o;
+    T o4 = T(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) o.v[m] = T(0);
 #pragma unroll
-    for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {  // taps 4 at a time (broadcast LDS reads)
+    for (int q4 = 0; q4 < ((PCS_ABL & 2048) ? 1 : (NQ + 3) / 4); ++q4) {  // taps 4 at a time (broadcast LDS reads)
       const G4<T> w4 = lds4(Wq + 32 + 4 * q4);
-      if (PCS_NM_SB) pcs_fence();
+      pcs_fence();
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int q = 4 * q4 + e;
         if (q < NQ) {
 #pragma unroll
           for (int m = 0; m < 4; ++m) o.v[m] += w4.v[e] * v[SHX + m + q];
+          o4 += w4.v[e] * v[SHX + 4 + q];
         }
       }
       pin4(o);
+      pin1(o4);
     }
     pcs_fence();
     if (PCS_NM_EDGE && c0 < H) {  // exact rows of N_h on the H columns nearest the left image edge
@@ -213,61 +224,73 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
         for (int m = 0; m < 4; ++m) o.v[m] -= (on ? e4.v[m] : T(0)) * xe[k];
       }
     }
-    if (PCS_NM_EDGE && c0 + TW > n1 - H) {  // ... and the right one (image columns n1 - 8 .. n1 - 1)
+    if (PCS_NM_EDGE && c0 + TW + 1 > n1 - H) {  // ... and the right one (image columns n1 - 8 .. n1 - 1)
       const T* xr8 = xrow + (n1 - 8 - xc0);
       const G4<T> x0 = lds4(xr8), x1 = lds4(xr8 + 4);
       const T xf[8] = {x0.v[0], x0.v[1], x0.v[2], x0.v[3], x1.v[0], x1.v[1], x1.v[2], x1.v[3]};
       const int j = ucg - (n1 - 8);
       const bool on = j == 0 || j == 4;
+      const bool on5 = ug == GG - 1 && ucg + 4 == n1 - 4;  // the 65th column is column n1 - 4
       const T* et = Wq + 64 + 24 * H + (on ? j : 0);
 #pragma unroll
       for (int k = 0; k < H; ++k) {
         const G4<T> e4 = lds4(et + 8 * k);
 #pragma unroll
         for (int m = 0; m < 4; ++m) o.v[m] -= (on ? e4.v[m] : T(0)) * xf[8 - H + k];
+        o4 -= (on5 ? et[8 * k + 4 - j] : T(0)) * xf[8 - H + k];
       }
     }
-    st4(TR + (lr & 63) * WT + 4 * ug, o);
+    T* trow = TR + (lr & 63) * WT + 4 * ug;
+    st4(trow, o);
+    if (ug == GG - 1) trow[4] = o4;
   };
-  // ---- PV + update: row lr = a + 1 + ui
-  auto pv = [&](int a, const G4<T>& bv, int ub) {
+  // ---- PV + update: row lr = a + 1 + ui, columns [c, c + 5) (the fifth: the last group's only)
+  auto pv = [&](int a, const G4<T>& bv, T b5, int ub) {
     const int lr = a + 1 + ui, gr = s.row0 + lr;
     int slot = ui + 1 + ub;
     slot = slot >= 17 ? slot - 17 : slot;
-    // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring.  The ring is 64 rows of 256 B, so the
-    // byte address of window row q is ((row bytes + 256 q) & 16383) | column bytes (2 VALU per
-    // read); reads are issued in chunks of PF behind a scheduling fence (at most 2 PF in flight)
+    // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring; window row q sits at p0 + q rows, or
+    // 64 rows earlier once the ring wraps (2 VALU per read); reads are issued in chunks of PF
+    // behind a compiler fence (at most 2 PF in flight)
     G4<T> g;
+    T g4 = T(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) g.v[m] = T(0);
-    const uint32_t rb0 = (uint32_t)((lr - 2 * H) & 63) * (WT * 4), cb = (uint32_t)ug * 16u;
-    const char* tbase = reinterpret_cast<const char*>(TR);
-    constexpr int PF = PCS_NM_PF, NCH = (NQ + PF - 1) / PF;  // window rows per chunk
+    const int sl0 = (lr - 2 * H) & 63, wrap = 64 - sl0;
+    const T* p0 = TR + sl0 * WT + 4 * ug;
+    const T* p1 = p0 - 64 * WT;
+    constexpr int PF = PCS_NM_PF, NCH = (PCS_ABL & 2048) ? 1 : (NQ + PF - 1) / PF;  // window rows per chunk
     G4<T> buf[2][PF];
-    auto rd = [&](int q) {
-      return lds4(reinterpret_cast<const T*>(tbase + (((rb0 + 256u * q) & 16383u) | cb)));
+    T buf4[2][PF];
+    auto rd = [&](int q, G4<T>& d, T& d4) {
+      const T* pq = (q < wrap ? p0 : p1) + q * WT;
+      d = lds4(pq);
+      d4 = lds1(pq + 4);
     };
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (j < NQ) buf[0][j] = rd(j);
+      if (j < NQ) rd(j, buf[0][j], buf4[0][j]);
     G4<T> w4;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (c + 1 < NCH) {
 #pragma unroll
         for (int j = 0; j < PF; ++j)
-          if ((c + 1) * PF + j < NQ) buf[(c + 1) & 1][j] = rd((c + 1) * PF + j);
+          if ((c + 1) * PF + j < NQ) rd((c + 1) * PF + j, buf[(c + 1) & 1][j], buf4[(c + 1) & 1][j]);
       }
       if ((c * PF) % 4 == 0) w4 = lds4(Wq + c * PF);  // the next 4 taps
       pcs_fence();
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         if (c * PF + j < NQ) {
+          const T w = w4.v[(c * PF + j) & 3];
 #pragma unroll
-          for (int m = 0; m < 4; ++m) g.v[m] += w4.v[(c * PF + j) & 3] * buf[c & 1][j].v[m];
+          for (int m = 0; m < 4; ++m) g.v[m] += w * buf[c & 1][j].v[m];
+          g4 += w * buf4[c & 1][j];
         }
       }
       pin4(g);  // the chunk's FMAs stay here (not sunk below the later reads)
+      pin1(g4);
       pcs_fence();
     }
     const int wrow0 = s.row0 + a + 1 + 4 * wv;  // the wave's first global row
@@ -277,45 +300,59 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
 #pragma unroll
       for (int k = 0; k < H; ++k) {
-        const G4<T> t4 = lds4(TR + ((kr0 + k) & 63) * WT + 4 * ug);
+        const T* tk = TR + ((kr0 + k) & 63) * WT + 4 * ug;
+        const G4<T> t4 = lds4(tk);
+        const T t5 = lds1(tk + 4);
         const T w = (top || bot) ? d[k] : T(0);
 #pragma unroll
         for (int m = 0; m < 4; ++m) g.v[m] -= w * t4.v[m];
+        g4 -= w * t5;
       }
     }
-    const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
+    const T* xrow = XR + (lr & 31) * WX + XL + 4 * ug;
+    const G4<T> xv4 = lds4(xrow);
+    const T xe = lds1(xrow + 4);
     const G4<T> za = lds4(Z0 + ui * WZ0 + 4 * ug);               // z0[lr - 1]
     const G4<T> zb = lds4(Z0 + (ui + 1) * WZ0 + 4 * ug);         // z0[lr]
     const G4<T> z1a = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug);        // z1[lr][c - 4 .. c - 1]
     const G4<T> z1b = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug + 4);    // z1[lr][c .. c + 3]
+    const T zae = lds1(Z0 + ui * WZ0 + 4 * ug + 4), zbe = lds1(Z0 + (ui + 1) * WZ0 + 4 * ug + 4);
+    const T z1e = lds1(Z1 + (ui + 1) * WZ1 + 4 * ug + 8);       // z1[lr][c + 4]
     const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
     const bool rrow = gr < n0 && lr <= s.rows;
     const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
     G4<T> uo, xo;
-    T sdx = T(0), sx = T(0);
+    T sdx = T(0), sx = T(0), ue;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const T gd = g.v[m] - bv.v[m];
-      const T xv = xv4.v[m];
-      // K^T z for forward differences, VStack order: (0 + D0^T z0) + D1^T z1
+    for (int m = 0; m < 5; ++m) {
+      const T gd = m < 4 ? g.v[m] - bv.v[m] : g4 - b5;
+      const T xv = m < 4 ? xv4.v[m] : xe;
+      // K^T z for forward differences, VStack order: (0 + D0^T z0) + D1^T z1; the fifth column
+      // (c + 4 = c0 + 64 for the last group) is never the image's last (n1 % 4 == 0)
       const T zl = (m == 0) ? z1a.v[3] : z1b.v[m - 1];
-      const T zr = z1b.v[m];
-      T d0 = r_first ? T(0) : za.v[m];
-      if (!r_last) d0 -= zb.v[m];
+      const T zr = m < 4 ? z1b.v[m] : z1e;
+      T d0 = r_first ? T(0) : (m < 4 ? za.v[m] : zae);
+      if (!r_last) d0 -= (m < 4 ? zb.v[m] : zbe);
       const T d1 = zl - ((m == 3 && clast) ? T(0) : zr);
       const T xt = prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
-      uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
-      const T xnew = P.rho * xt + P.omr * xv;
-      xo.v[m] = xnew;
-      const T dx = xv - xnew;
-      sdx += dx * dx;
-      sx += xv * xv;
+      if (m < 4) {
+        uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
+        const T xnew = P.rho * xt + P.omr * xv;
+        xo.v[m] = xnew;
+        const T dx = xv - xnew;
+        sdx += dx * dx;
+        sx += xv * xv;
+      } else {
+        ue = (rrow && ucg + 4 < n1) ? (T(2) * xt - xv) : T(0);
+      }
     }
     if (own) {
       part[0] += (double)sdx;
       part[1] += (double)sx;
     }
-    st4(U + slot * WU + 4 * ug, uo);
+    T* urow = U + slot * WU + 4 * ug;
+    st4(urow, uo);
+    if (ug == GG - 1) urow[4] = ue;
     bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
   };
   // ---- P6: z' on row lr = a + ui
@@ -366,7 +403,10 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   };
 
   // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0
+  // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5)
+  const uint32_t co_b5 = ug == GG - 1 ? col_off(c0 + TW, n1) : kOOB;
   G4<T> xnx[KXN], bv;
+  T b5;
   {
     G4<T> xv[KXP];
 #pragma unroll
@@ -377,6 +417,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     }
     load_z(s0 - TS, TS - 1);  // z rows s0 - 1, s0 only (the prologue's one update row), b on row s0
     bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
+    b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
 #pragma unroll
     for (int k = 0; k < KXP; ++k) {
       if (!PCS_WAVE_ON(k, M::NXP)) continue;
@@ -390,8 +431,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   ph(s0 - 2 * H + ui);  // t rows [s0 - 2H, s0 - 2H + 16)
   if (ui + TS < 4 * H + 1) ph(s0 - 2 * H + TS + ui);  // t rows [s0 - 2H + 16, s0 + 2H]
   lds_barrier();
-  if (wv == 3) pv(s0 - TS, bv, 1);  // u on row s0 -> u ring slot 0, x' on row s0 (rows above: not own)
-  load_xn(xnx, s0 + 2 * H + 1);     // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
+  if (wv == 3) pv(s0 - TS, bv, b5, 1);  // u on row s0 -> u ring slot 0, x' on row s0 (rows above: not own)
+  load_xn(xnx, s0 + 2 * H + 1);        // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
   lds_barrier();
   store_xn(xnx, s0 + 2 * H + 1);  // slots of rows [s0 + 2H - 31, s0 + 2H - 15): read by PH above only
 
@@ -404,12 +445,14 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     asm volatile("" : "+v"(Wq));
     // this step's z tiles (LDS-DMA) and b, the next step's x rows (registers, landed after P6)
     load_z(a, 0);
-    bv = bload4(vb.r, vb.row_off(a + 1 + ui) + co_u);
+    const uint32_t rb = vb.row_off(a + 1 + ui);
+    bv = bload4(vb.r, rb + co_u);
+    b5 = bload4(vb.r, rb + co_b5).v[0];
     load_xn(xnx, a + 2 * H + 1 + TS);
     ph(a + 2 * H + 1 + ui);
-    vm_wait<KXN + 1>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
+    vm_wait<KXN + 2>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
-    pv(a, bv, ub);
+    pv(a, bv, b5, ub);
     lds_barrier();
     p6(a, ub);
     store_xn(xnx, a + 2 * H + 1 + TS);  // x ring slots of rows [a + 2H - 15, a + 2H + 1): read above
@@ -419,7 +462,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #undef PCS_ITEM
 }
 
-// One block per task (60-column strip x row segment); with `hist` the last workgroups also
+// One block per task (64-column strip x row segment); with `hist` the last workgroups also
 // reduce the partials and run the loop control, with `ro.sums` they only reduce.
 template <typename T, int H, int HK, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))) void k_pds2d_nmarch(
@@ -443,7 +486,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
   int s0, s1;
   band_rows(bd, seg, s0, s1);
-  const int c0 = strip * M::TO;
+  const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   if (!stopped) nmarch_task<T, H, HK, NT>(x, xn, z, zn, b, tq, s, P, gk, s0, s1, c0, sm, zs0, zs1, part);

@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib as L
+from ..opt.engine import nmarch_taps
 from .. import _ops as O
 
 
@@ -353,6 +354,15 @@ class SlabPDS2D:
         if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV):
             self.y = lay.window(-O.to_dev(spec['shift'], dtype), hy)  # y = -shift, exactly
             a.y = self.y.data_ptr()
+        if (fk == L.PCS_F_SEPCONV and dtype == torch.float32 and half <= 7
+                and os.environ.get('PCS_NMARCH', '1') != '0'):
+            # normal-operator march kernel (as PDS2DEngine): Conv^T y of the global image in fp64,
+            # this rank's window of it (own rows + the y halo)
+            self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+            cty = spec['conv']._adj(-O.to_dev(spec['shift'], torch.float64)).to(dtype)
+            self.cty = lay.window(cty, hy).contiguous()
+            del cty
+            a.cty, a.ntaps = self.cty.data_ptr(), self.ntaps.data_ptr()
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
         a.partials = self.partials.data_ptr()

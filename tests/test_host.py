@@ -147,3 +147,44 @@ def test_pds2d_reduce_only_argument_checks():
     a.pre_partials = None
     assert lib.pcs_pds2d_step(ctypes.byref(a), None) == -1
     assert lib.pcs_pds2d_step_bands(ctypes.byref(a), 0, 8, 56, 64, None) == -1
+
+
+@pytest.mark.parametrize('half', [7, 5, 3, 2])
+def test_nmarch_tables_equal_dense_normal_operator(half):
+    """The normal-operator march kernel's tables (pycsou_amd.opt.engine.nmarch_taps) rebuild
+    N = C^T C of the zero-boundary 'same' 1-D convolution along each axis exactly (fp32 table
+    rounding): window taps away from the edges, window - E on the H samples nearest each edge,
+    zero outside the 4H+1 band."""
+    from pycsou_amd.opt.engine import nmarch_taps
+    H = 3 if half <= 3 else 7
+    r = np.arange(2 * half + 1) - half
+    t0 = np.exp(-0.5 * (r / 2.0) ** 2)
+    t0 /= t0.sum()
+    t1 = np.exp(-0.5 * (r / 1.3) ** 2) * (1 + 0.1 * r)
+    t1 /= t1.sum()
+    tab = nmarch_taps(t0, t1, half).astype(np.float64)
+    assert tab.size == 64 + 32 * H
+    n = 40
+    for t, axis in ((t0, 0), (t1, 1)):
+        C = np.zeros((n, n))
+        for i in range(n):
+            for j in range(max(0, i - half), min(n, i + half + 1)):
+                C[i, j] = t[half + i - j]
+        N = C.T @ C
+        win = tab[32 * axis:32 * axis + 4 * H + 1]
+        M = np.zeros((n, n))
+        for j in range(n):
+            for k in range(max(0, j - 2 * H), min(n, j + 2 * H + 1)):
+                v = win[k - j + 2 * H]
+                if axis == 0:
+                    if j < H and k < H:
+                        v -= tab[64 + 8 * j + k]
+                    if j >= n - H and k >= n - H:
+                        v -= tab[64 + 8 * H + 8 * (j - (n - H)) + (k - (n - H))]
+                else:  # transposed right/left tables, as the kernel indexes them
+                    if j < H and k < H:
+                        v -= tab[64 + 16 * H + 8 * k + j]
+                    if j >= n - H and k >= n - H:
+                        v -= tab[64 + 24 * H + 8 * (k - (n - H)) + (8 - H) + (j - (n - H))]
+                M[j, k] = v
+        np.testing.assert_allclose(M, N, atol=2e-8)

@@ -50,7 +50,7 @@ def child():
         b2b(50)
     iso = eng.time_step_kernel(100)
     bb = min(b2b(N) for _ in range(3))
-    print(f'RESULT {iso * 1e3:.1f} {bb * 1e3:.1f}', flush=True)
+    print(f'RESULT {iso * 1e3:.1f} {bb * 1e3:.1f} {eng.nblocks}', flush=True)
 
 
 def main():
@@ -71,9 +71,9 @@ def main():
             if not line:
                 print(k, 'FAILED', out.stderr[-2000:], flush=True)
                 return 1
-            iso, bb = map(float, line[0].split()[1:])
+            iso, bb, nbk = map(float, line[0].split()[1:])
             res[k].append((iso, bb))
-            print(f'{k:>10s} rep {rep}: isolated {iso:6.1f} us  back-to-back {bb:6.1f} us', flush=True)
+            print(f'{k:>10s} rep {rep}: isolated {iso:6.1f} us  back-to-back {bb:6.1f} us  ({nbk:.0f} workgroups)', flush=True)
     for k, r in res.items():
         print(f'{k:>10s} best: isolated {min(i for i, _ in r):6.1f} us  back-to-back {min(b for _, b in r):6.1f} us')
     return 0

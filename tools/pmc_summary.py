@@ -2,7 +2,7 @@
 import csv, sys, collections, glob
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[1:]:
-    for f in glob.glob(path):
+    for f in glob.glob(path, recursive=True):
         for r in csv.DictReader(open(f)):
             k = r['Kernel_Name'][:60]
             vals[k][r['Counter_Name']].append(float(r['Counter_Value']))
