@@ -118,6 +118,7 @@ static Params<T> make_params(const pcs_pds2d_args* a) {
   const double t_h = (1.0 / a->sigma) * a->lam;  // ProxFuncPostComp: tau*scale with tau = 1/sigma
   P.t_h = (T)t_h;
   P.inv_t_h = (T)(1.0 / t_h);
+  P.lam = (T)a->lam;
   P.inv_step0 = (T)(1.0 / a->step0);
   P.inv_step1 = (T)(1.0 / a->step1);
   P.unit0 = a->step0 == 1.0;

@@ -79,7 +79,9 @@ struct NMarch {
   static constexpr int XL = RU4<2 * H>::value, SHX = XL - 2 * H;  // x region [c0 - XL, c0 + TW + XL)
   static constexpr int GXL = (TW + 2 * XL) / 4;                    // loaded x groups per row (24 / 20)
   static constexpr int WX = TW + 2 * XL + 4;                       // x ring pitch (odd slot count)
-  static constexpr int XRING = 32, TRING = 64;
+  // t ring: 48 rows (a step's window + new rows: 4H + 2 TS <= 48 + TS) + a mirror of its first 4H
+  // (rows 48..48+4H-1 repeat rows 0..4H-1), so any (4H+1)-row window starting in the ring is contiguous
+  static constexpr int XRING = 32, TRING = 48, TMIR = 4 * H;
   static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B)
   // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 16 groups, z1 rows
   // of 17 groups (from column c0 - 4); 5 wave-instructions of 64 x 16 B each
@@ -87,12 +89,13 @@ struct NMarch {
   static constexpr int NVH = (SHX + 3 + 4 * H) / 4 + 1;  // b128 groups a PH item reads
   static constexpr int NXN = TS * GXL;                   // x items per step
   static constexpr int NXP = (4 * H + 1) * GXL;          // prologue x items
-  static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + TRING * WT, O_W = O_U + (TS + 1) * WU,
+  static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + (TRING + TMIR) * WT, O_W = O_U + (TS + 1) * WU,
                        NW = 64 + 32 * H, SZ = O_W + NW;  // W: the ntaps table
   static_assert((TS + 1) * (WZ0 / 4) <= ZSLOTS && (TS + 1) * (WZ1 / 4) <= ZSLOTS, "z tiles");
   static_assert(H == 3 || H == 7, "tiers 3 and 7");
   static_assert(TS + 2 * H + 1 + TS <= XRING + 1 + 2 * H, "x ring holds rows [a+1, a+2H+17)");
-  static_assert(2 * (2 * H) + TS <= TRING - TS, "t ring: the rows PH writes never hold a row PV reads");
+  static_assert(4 * H + TS <= TRING, "t ring holds a step's PV window (the rows PH writes are its newest)");
+  static __device__ __forceinline__ int tslot(int r) { return (int)((unsigned)(r + TRING * (1 << 20)) % TRING); }
   static_assert(4 * (NVH - 1) + 3 >= SHX + 4 + 4 * H, "PH window (5 outputs)");
   static_assert((WX / 4) % 2 == 1, "odd x slot pitch");
 };
@@ -112,7 +115,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   T* TR = sm + M::O_T;
   T* U = sm + M::O_U;
   T* W = sm + M::O_W;  // taps (broadcast reads, re-read per phase: none live across the loop)
-  const T* Wq = W;     // the taps' address, laundered every step (no loop-invariant tap reads)
+  int wz = 0;          // 0, laundered every step: taps read at W + wz are not loop-invariant
+  const T* Wq = W;     // (so no tap read is hoisted out of the loop into registers)
   for (int i = threadIdx.x; i < M::NW; i += NT) W[i] = tq[i];  // visible after the first barrier
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -240,30 +244,33 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
         o4 -= (on5 ? et[8 * k + 4 - j] : T(0)) * xf[8 - H + k];
       }
     }
-    T* trow = TR + (lr & 63) * WT + 4 * ug;
+    const int sl = M::tslot(lr);
+    T* trow = TR + sl * WT + 4 * ug;
     st4(trow, o);
     if (ug == GG - 1) trow[4] = o4;
+    if (sl < M::TMIR) {  // the mirror copy
+      st4(trow + M::TRING * WT, o);
+      if (ug == GG - 1) trow[M::TRING * WT + 4] = o4;
+    }
   };
   // ---- PV + update: row lr = a + 1 + ui, columns [c, c + 5) (the fifth: the last group's only)
   auto pv = [&](int a, const G4<T>& bv, T b5, int ub) {
     const int lr = a + 1 + ui, gr = s.row0 + lr;
     int slot = ui + 1 + ub;
     slot = slot >= 17 ? slot - 17 : slot;
-    // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring; window row q sits at p0 + q rows, or
-    // 64 rows earlier once the ring wraps (2 VALU per read); reads are issued in chunks of PF
-    // behind a compiler fence (at most 2 PF in flight)
+    // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring, window row q at p0 + q rows (no
+    // address arithmetic: immediate offsets); reads are issued in chunks of PF behind a compiler
+    // fence (at most 2 PF in flight)
     G4<T> g;
     T g4 = T(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) g.v[m] = T(0);
-    const int sl0 = (lr - 2 * H) & 63, wrap = 64 - sl0;
-    const T* p0 = TR + sl0 * WT + 4 * ug;
-    const T* p1 = p0 - 64 * WT;
+    const T* p0 = TR + M::tslot(lr - 2 * H) * WT + 4 * ug;  // the window is contiguous (mirror rows)
     constexpr int PF = PCS_NM_PF, NCH = (PCS_ABL & 2048) ? 1 : (NQ + PF - 1) / PF;  // window rows per chunk
     G4<T> buf[2][PF];
     T buf4[2][PF];
     auto rd = [&](int q, G4<T>& d, T& d4) {
-      const T* pq = (q < wrap ? p0 : p1) + q * WT;
+      const T* pq = p0 + q * WT;
       d = lds4(pq);
       d4 = lds1(pq + 4);
     };
@@ -300,7 +307,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
 #pragma unroll
       for (int k = 0; k < H; ++k) {
-        const T* tk = TR + ((kr0 + k) & 63) * WT + 4 * ug;
+        const T* tk = TR + (M::tslot(kr0) + k) * WT + 4 * ug;  // contiguous through the mirror
         const G4<T> t4 = lds4(tk);
         const T t5 = lds1(tk + 4);
         const T w = (top || bot) ? d[k] : T(0);
@@ -376,16 +383,15 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const T d0 = r_last ? T(0) : (ud.v[m] - uc.v[m]);
       const T d1 = (m == 3 && clast) ? T(0) : (uright - uc.v[m]);
       const T w0v = zv0.v[m] + P.sigma * (d0 * P.inv_step0), w1v = zv1.v[m] + P.sigma * (d1 * P.inv_step1);
-      const T v0 = w0v * P.inv_sigma, v1 = w1v * P.inv_sigma;
       T zt0, zt1;
-      if (HK == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
-        T f = T(1) - P.t_h * fast_rsqrt(v0 * v0 + v1 * v1);
-        f = f > T(0) ? f : T(0);
-        zt0 = w0v - P.sigma * (f * v0);
-        zt1 = w1v - P.sigma * (f * v1);
-      } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
-        zt0 = w0v - P.sigma * (v0 - P.t_h * clip1(v0 * P.inv_t_h));
-        zt1 = w1v - P.sigma * (v1 - P.t_h * clip1(v1 * P.inv_t_h));
+      if (HK == PCS_H_L21) {
+        // w - sigma prox_{L21, t}(w / sigma) (penalty.py:551-557, t = lam / sigma) = w min(1, lam / ||w||)
+        const T sc = fminf(T(1), P.lam * fast_rsqrt(w0v * w0v + w1v * w1v));
+        zt0 = w0v * sc;
+        zt1 = w1v * sc;
+      } else {  // w - sigma (v - t clip(v / t)), v = w / sigma (func/base.py:239-240) = clip(w, -lam, lam)
+        zt0 = fminf(fmaxf(w0v, -P.lam), P.lam);
+        zt1 = fminf(fmaxf(w1v, -P.lam), P.lam);
       }
       o0.v[m] = P.rho * zt0 + P.omr * zv0.v[m];
       o1.v[m] = P.rho * zt1 + P.omr * zv1.v[m];
@@ -442,7 +448,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
     lds_barrier();  // step k-1 done with U, Z and the t / x ring rows it read; its x rows landed
-    asm volatile("" : "+v"(Wq));
+    asm volatile("" : "+v"(wz));
+    Wq = W + wz;
     // this step's z tiles (LDS-DMA) and b, the next step's x rows (registers, landed after P6)
     load_z(a, 0);
     const uint32_t rb = vb.row_off(a + 1 + ui);

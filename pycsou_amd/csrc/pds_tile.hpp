@@ -177,6 +177,7 @@ __device__ __forceinline__ void col_item(const T* __restrict__ in, int pin, int 
 template <typename T>
 struct Params {
   T tau, sigma, inv_sigma, rho, omr, t_h, inv_t_h, inv_step0, inv_step1, seg_a, seg_b;
+  T lam;  // H = lam * L1 / L21 (the normal-operator kernel's fenchel step: clip / scale by lam)
   int unit0, unit1;  // step == 1: skip the scaling (exact)
 };
 
