@@ -47,7 +47,7 @@ import torch.distributed as dist
 
 METRIC = 'PDS iters/sec on 4096² TV-deconv; achieved HBM GB/s vs roofline at 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-TRAFFIC_JSON = 'profiles/r1_traffic.json'  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the step kernel (tools/prof_run.sh)
+TRAFFIC_JSON = 'profiles/r2_nm_traffic.json'  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the step kernel (tools/prof_nm.sh)
 
 
 def phantom(shape, n_rect, seed):
@@ -332,7 +332,7 @@ def fused_2d(pds, dtype, K, W, chunk=32):
     # timed region; the rocprofv3 kernel-trace averages in profiles/ must agree)
     kern = eng.time_iteration_kernels(min(max(K, 20), 100))
     res = {'ms_per_step': ms, 'kernels_ms': kern, 'nblocks': eng.nblocks, 'native': eng.native,
-           'fkind': int(eng.fkind)}
+           'fkind': int(eng.fkind), 'nmarch': getattr(eng, 'cty', None) is not None}
     del eng
     torch.cuda.empty_cache()
     return res
@@ -532,7 +532,8 @@ def main():
         achieved = alg_bytes / (res['kernel_ms'] * 1e-3) / 1e9
         traffic, tsrc = None, None
         tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON)
-        if os.path.exists(tpath) and dtype == torch.float32 and n == 4096:
+        nm = res.get('nmarch', False)
+        if os.path.exists(tpath) and dtype == torch.float32 and n == 4096 and nm:
             traffic = round(json.load(open(tpath))['traffic_bytes'])  # PMC FETCH/WRITE per launch (corrected)
             tsrc = TRAFFIC_JSON
         out = {
@@ -554,14 +555,17 @@ def main():
             'steps_requested': args.steps, 'warmup_requested': args.warmup,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,
-                         'kernel': 'pcs_pds2d_step (k_pds2d_march<float,7,L21,256>)',
+                         'kernel': ('pcs_pds2d_step (k_pds2d_nmarch<float,7,L21,256>: grad F = N x - Conv^T y, '
+                                    'N = Conv^T Conv as two 29-tap passes)' if nm else
+                                    'pcs_pds2d_step (k_pds2d_march<float,7,L21,256>)'),
                          'kernel_ms': round(res['kernel_ms'], 5),
                          'kernel_ms_source': 'median of HIP-event pairs around each of 100 isolated launches',
                          'alg_bytes_per_launch': alg_bytes,
-                         # the 15x15 PSF work beside the bandwidth figure -- the separable
-                         # passes (2 x 15 taps forward, 2 x 15 adjoint, 2 flop each) per pixel
-                         'conv_flop_per_launch': 120 * N,
-                         'conv_tflops': round(120 * N / (res['kernel_ms'] * 1e-3) / 1e12, 2),
+                         # the 15x15 PSF work beside the bandwidth figure -- per pixel the
+                         # normal operator's two 29-tap passes (nmarch) or the four 15-tap separable
+                         # passes (2 flop per tap)
+                         'conv_flop_per_launch': (116 if nm else 120) * N,
+                         'conv_tflops': round((116 if nm else 120) * N / (res['kernel_ms'] * 1e-3) / 1e12, 2),
                          'fp32_vector_peak_tflops': 157.3},
             'iteration_GBps': round(alg_bytes / (ms * 1e-3) / 1e9, 1),
         }

@@ -253,7 +253,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       if (ug == GG - 1) trow[M::TRING * WT + 4] = o4;
     }
   };
-  // ---- PV + update: row lr = a + 1 + ui, columns [c, c + 5) (the fifth: the last group's only)
+  // ---- PV + update: row lr = a + 1 + ui, columns [c, c + 4); the last group also column c + 4
+  // (the strip's 65th), in a branch of its own lanes (4 per wave: conflict-free b32 reads)
   auto pv = [&](int a, const G4<T>& bv, T b5, int ub) {
     const int lr = a + 1 + ui, gr = s.row0 + lr;
     int slot = ui + 1 + ub;
@@ -262,96 +263,77 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     // address arithmetic: immediate offsets); reads are issued in chunks of PF behind a compiler
     // fence (at most 2 PF in flight)
     G4<T> g;
-    T g4 = T(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) g.v[m] = T(0);
     const T* p0 = TR + M::tslot(lr - 2 * H) * WT + 4 * ug;  // the window is contiguous (mirror rows)
     constexpr int PF = PCS_NM_PF, NCH = (PCS_ABL & 2048) ? 1 : (NQ + PF - 1) / PF;  // window rows per chunk
     G4<T> buf[2][PF];
-    T buf4[2][PF];
-    auto rd = [&](int q, G4<T>& d, T& d4) {
-      const T* pq = p0 + q * WT;
-      d = lds4(pq);
-      d4 = lds1(pq + 4);
-    };
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (j < NQ) rd(j, buf[0][j], buf4[0][j]);
+      if (j < NQ) buf[0][j] = lds4(p0 + j * WT);
     G4<T> w4;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (c + 1 < NCH) {
 #pragma unroll
         for (int j = 0; j < PF; ++j)
-          if ((c + 1) * PF + j < NQ) rd((c + 1) * PF + j, buf[(c + 1) & 1][j], buf4[(c + 1) & 1][j]);
+          if ((c + 1) * PF + j < NQ) buf[(c + 1) & 1][j] = lds4(p0 + ((c + 1) * PF + j) * WT);
       }
       if ((c * PF) % 4 == 0) w4 = lds4(Wq + c * PF);  // the next 4 taps
       pcs_fence();
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         if (c * PF + j < NQ) {
-          const T w = w4.v[(c * PF + j) & 3];
 #pragma unroll
-          for (int m = 0; m < 4; ++m) g.v[m] += w * buf[c & 1][j].v[m];
-          g4 += w * buf4[c & 1][j];
+          for (int m = 0; m < 4; ++m) g.v[m] += w4.v[(c * PF + j) & 3] * buf[c & 1][j].v[m];
         }
       }
       pin4(g);  // the chunk's FMAs stay here (not sunk below the later reads)
-      pin1(g4);
       pcs_fence();
     }
     const int wrow0 = s.row0 + a + 1 + 4 * wv;  // the wave's first global row
-    if (PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H)) {  // the exact rows of N_v on the H rows nearest an image edge
-      const bool top = gr >= 0 && gr < H, bot = gr >= n0 - H && gr < n0;
-      const T* d = Wq + 64 + (top ? 8 * gr : 8 * H + 8 * (gr - (n0 - H)));
-      const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
+    const bool vedge = PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H);  // rows of N_v near an image edge
+    const bool top = gr >= 0 && gr < H, bot = gr >= n0 - H && gr < n0;
+    const T* d = Wq + 64 + (top ? 8 * gr : 8 * H + 8 * (gr - (n0 - H)));
+    const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
+    if (vedge) {
 #pragma unroll
       for (int k = 0; k < H; ++k) {
-        const T* tk = TR + (M::tslot(kr0) + k) * WT + 4 * ug;  // contiguous through the mirror
-        const G4<T> t4 = lds4(tk);
-        const T t5 = lds1(tk + 4);
+        const G4<T> t4 = lds4(TR + (M::tslot(kr0) + k) * WT + 4 * ug);  // contiguous through the mirror
         const T w = (top || bot) ? d[k] : T(0);
 #pragma unroll
         for (int m = 0; m < 4; ++m) g.v[m] -= w * t4.v[m];
-        g4 -= w * t5;
       }
     }
-    const T* xrow = XR + (lr & 31) * WX + XL + 4 * ug;
-    const G4<T> xv4 = lds4(xrow);
-    const T xe = lds1(xrow + 4);
+    const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
     const G4<T> za = lds4(Z0 + ui * WZ0 + 4 * ug);               // z0[lr - 1]
     const G4<T> zb = lds4(Z0 + (ui + 1) * WZ0 + 4 * ug);         // z0[lr]
     const G4<T> z1a = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug);        // z1[lr][c - 4 .. c - 1]
     const G4<T> z1b = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug + 4);    // z1[lr][c .. c + 3]
-    const T zae = lds1(Z0 + ui * WZ0 + 4 * ug + 4), zbe = lds1(Z0 + (ui + 1) * WZ0 + 4 * ug + 4);
-    const T z1e = lds1(Z1 + (ui + 1) * WZ1 + 4 * ug + 8);       // z1[lr][c + 4]
     const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
     const bool rrow = gr < n0 && lr <= s.rows;
     const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+    // x_t = prox_G((x - tau g) - tau K^T z); K^T z for forward differences, VStack order:
+    // (0 + D0^T z0) + D1^T z1
+    auto xt_of = [&](T gd, T xv, T za_, T zb_, T zl, T zr, bool last_col) {
+      T d0 = r_first ? T(0) : za_;
+      if (!r_last) d0 -= zb_;
+      const T d1 = zl - (last_col ? T(0) : zr);
+      return prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
+    };
     G4<T> uo, xo;
-    T sdx = T(0), sx = T(0), ue;
+    T sdx = T(0), sx = T(0);
 #pragma unroll
-    for (int m = 0; m < 5; ++m) {
-      const T gd = m < 4 ? g.v[m] - bv.v[m] : g4 - b5;
-      const T xv = m < 4 ? xv4.v[m] : xe;
-      // K^T z for forward differences, VStack order: (0 + D0^T z0) + D1^T z1; the fifth column
-      // (c + 4 = c0 + 64 for the last group) is never the image's last (n1 % 4 == 0)
-      const T zl = (m == 0) ? z1a.v[3] : z1b.v[m - 1];
-      const T zr = m < 4 ? z1b.v[m] : z1e;
-      T d0 = r_first ? T(0) : (m < 4 ? za.v[m] : zae);
-      if (!r_last) d0 -= (m < 4 ? zb.v[m] : zbe);
-      const T d1 = zl - ((m == 3 && clast) ? T(0) : zr);
-      const T xt = prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
-      if (m < 4) {
-        uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
-        const T xnew = P.rho * xt + P.omr * xv;
-        xo.v[m] = xnew;
-        const T dx = xv - xnew;
-        sdx += dx * dx;
-        sx += xv * xv;
-      } else {
-        ue = (rrow && ucg + 4 < n1) ? (T(2) * xt - xv) : T(0);
-      }
+    for (int m = 0; m < 4; ++m) {
+      const T xv = xv4.v[m];
+      const T xt = xt_of(g.v[m] - bv.v[m], xv, za.v[m], zb.v[m], (m == 0) ? z1a.v[3] : z1b.v[m - 1], z1b.v[m],
+                         m == 3 && clast);
+      uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
+      const T xnew = P.rho * xt + P.omr * xv;
+      xo.v[m] = xnew;
+      const T dx = xv - xnew;
+      sdx += dx * dx;
+      sx += xv * xv;
     }
     if (own) {
       part[0] += (double)sdx;
@@ -359,8 +341,26 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     }
     T* urow = U + slot * WU + 4 * ug;
     st4(urow, uo);
-    if (ug == GG - 1) urow[4] = ue;
     bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+    if (ug == GG - 1) {  // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0)
+      const T* q0 = p0 + 4;
+      T g4 = T(0);
+#pragma unroll
+      for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {
+        const G4<T> w = lds4(Wq + 4 * q4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * q4 + e < NQ) g4 += w.v[e] * lds1(q0 + (4 * q4 + e) * WT);
+      }
+      if (vedge) {
+#pragma unroll
+        for (int k = 0; k < H; ++k) g4 -= ((top || bot) ? d[k] : T(0)) * lds1(TR + (M::tslot(kr0) + k) * WT + TW);
+      }
+      const T xe = lds1(XR + (lr & 31) * WX + XL + TW);
+      const T xt = xt_of(g4 - b5, xe, lds1(Z0 + ui * WZ0 + TW), lds1(Z0 + (ui + 1) * WZ0 + TW), z1b.v[3],
+                         lds1(Z1 + (ui + 1) * WZ1 + TW + 4), false);
+      urow[4] = (rrow && ucg + 4 < n1) ? (T(2) * xt - xe) : T(0);
+    }
   };
   // ---- P6: z' on row lr = a + ui
   auto p6 = [&](int a, int ub) {
@@ -372,7 +372,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     const G4<T> ud = lds4(U + sl1 * WU + 4 * ug);
     const G4<T> zv0 = lds4(Z0 + ui * WZ0 + 4 * ug);
     const G4<T> zv1 = lds4(Z1 + ui * WZ1 + 4 * ug + 4);
-    const T une = U[sl0 * WU + 4 * ug + 4];
+    const T une = lds4(U + sl0 * WU + 4 * ug + 4).v[0];  // u[c + 4] (a b128 read: conflict-free)
     const bool r_last = gr >= n0 - 1;
     const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
     G4<T> o0, o1;

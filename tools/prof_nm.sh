@@ -14,5 +14,5 @@ timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc4 -o run --output-format
 f3=$(find $OUT/pmc3 -name '*counter_collection.csv' | head -1); f4=$(find $OUT/pmc4 -name '*counter_collection.csv' | head -1)
 python3 tools/traffic_from_pmc.py $f3 $f4 $OUT/traffic.json $K > /dev/null || exit 16
 python3 tools/pmc_summary.py "$OUT/pmc*/**/*counter_collection.csv" > $OUT/pmc_summary.txt 2>&1 || true
-find $OUT -name '*kernel_trace.csv' -delete
+find $OUT -name "*kernel_trace.csv" -delete; find $OUT -name "*counter_collection.csv" -delete; find $OUT -name "*agent_info.csv" -delete
 echo prof_ok
