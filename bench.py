@@ -541,7 +541,7 @@ def main():
             'ms_per_step': round(ms, 5), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': args.dtype, 'data': 'synthetic',
             'config': {'workload': f'C3 TV-deconvolution {n}x{n} per GPU ({n * world}x{n} global, row slabs), '
-                                   f'15x15 Gaussian PSF sigma=2 (rank-1: separable passes), isotropic TV '
+                                   f'15x15 Gaussian PSF sigma=2 (rank-1: grad F = N x - Conv^T y, N = Conv^T Conv as two 29-tap passes), isotropic TV '
                                    f'0.05*L21Norm, Gradient(kind=forward), PDS fused step, '
                                    + ('iterations launched back to back from C (pcs_pds2d_run)'
                                       if 'nblocks' in res and world == 1
