@@ -199,23 +199,27 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     T o4 = T(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) o.v[m] = T(0);
+    // taps 4 at a time (broadcast LDS reads), the next 4 read while the current ones are used
+    constexpr int NQ4 = (PCS_ABL & 2048) ? 1 : (NQ + 3) / 4;
+    G4<T> wc = lds4(Wq + 32), wn;
 #pragma unroll
-    for (int q4 = 0; q4 < ((PCS_ABL & 2048) ? 1 : (NQ + 3) / 4); ++q4) {  // taps 4 at a time (broadcast LDS reads)
-      const G4<T> w4 = lds4(Wq + 32 + 4 * q4);
+    for (int q4 = 0; q4 < NQ4; ++q4) {
+      if (q4 + 1 < NQ4) wn = lds4(Wq + 32 + 4 * (q4 + 1));
       pcs_fence();
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int q = 4 * q4 + e;
         if (q < NQ) {
 #pragma unroll
-          for (int m = 0; m < 4; ++m) o.v[m] += w4.v[e] * v[SHX + m + q];
-          o4 += w4.v[e] * v[SHX + 4 + q];
+          for (int m = 0; m < 4; ++m) o.v[m] += wc.v[e] * v[SHX + m + q];
+          o4 += wc.v[e] * v[SHX + 4 + q];
         }
       }
       pin4(o);
       pin1(o4);
+      pcs_fence();
+      wc = wn;
     }
-    pcs_fence();
     if (PCS_NM_EDGE && c0 < H) {  // exact rows of N_h on the H columns nearest the left image edge
       const G4<T> x0 = lds4(xrow + XL), x1 = lds4(xrow + XL + 4);  // image columns 0..7
       const T xe[8] = {x0.v[0], x0.v[1], x0.v[2], x0.v[3], x1.v[0], x1.v[1], x1.v[2], x1.v[3]};
@@ -271,15 +275,17 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #pragma unroll
     for (int j = 0; j < PF; ++j)
       if (j < NQ) buf[0][j] = lds4(p0 + j * WT);
-    G4<T> w4;
+    // taps 4 at a time, the next 4 read one chunk ahead of their use (as the window rows)
+    static_assert(4 % PF == 0, "a tap group spans whole chunks");
+    G4<T> w4 = lds4(Wq), w4n;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (c + 1 < NCH) {
 #pragma unroll
         for (int j = 0; j < PF; ++j)
           if ((c + 1) * PF + j < NQ) buf[(c + 1) & 1][j] = lds4(p0 + ((c + 1) * PF + j) * WT);
+        if (((c + 1) * PF) % 4 == 0) w4n = lds4(Wq + (c + 1) * PF);
       }
-      if ((c * PF) % 4 == 0) w4 = lds4(Wq + c * PF);  // the next 4 taps
       pcs_fence();
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
@@ -290,6 +296,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       }
       pin4(g);  // the chunk's FMAs stay here (not sunk below the later reads)
       pcs_fence();
+      if (c + 1 < NCH && ((c + 1) * PF) % 4 == 0) w4 = w4n;
     }
     const int wrow0 = s.row0 + a + 1 + 4 * wv;  // the wave's first global row
     const bool vedge = PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H);  // rows of N_v near an image edge
