@@ -21,6 +21,8 @@
 // sum_t h'[t] in[j + o - t], h'[t] = h[t - pad], o = off + pad); the adjoint passes use
 // h'[14 - t] with offset 14 - o.  Persistent grid, tasks (plane, row segment, strip) with the
 // strip fastest and an XCD-aware task map, as k_sep2d_march.
+#include <cstring>
+
 #include "vecio.hpp"
 
 namespace pcs {
@@ -306,6 +308,378 @@ static int ata_padb(int kb, int offb) {
   return -1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same operator as TWO 29-tap passes (the default when the taps reach <= 7 samples either
+// side and the plane is >= 16 x 16): per axis C^T C is the autocorrelation of the taps,
+//   (C^T C)[j, k] = a[j - k] - E[j][k],  a[e] = sum_m c(m) c(m + e),  c(d) = h[d + off],
+// E the terms of the samples outside the plane (rows i < 0 / i >= n), nonzero only for j, k in
+// the 7 samples nearest each edge (the zero boundary of the reference's Convolve1D, PyLops 1.x
+// `Convolve1D` truncation between C and C^T).  A 128-column (fp32) / 64-column (fp64) strip
+// marches down a row segment 32 rows per step:
+//   PH  horizontal 29-tap pass of the 32 staged input rows (+ the left / right edge terms)
+//       -> a ring of RS + 28 rows (each input row filtered once: no vertical halo recomputed)
+//   PV  vertical 29-tap pass, RB rows x 4 columns per thread (RB + 28 ring reads per 4 RB
+//       outputs) + the top / bottom edge terms -> HBM
+// Two barriers per step; the next step's input rows are in flight (registers) during PH and PV.
+// The tables (a for both axes, the four 7x7 edge blocks) are built per workgroup from the taps
+// in fp64.  2 words of HBM traffic per voxel, like one k_sep2d_march pass, for the work of two.
+// diagnostic ablation builds only (-DPCS_NRM_ABL=bits, tools/build_var.sh): 1 = output stores
+// dropped, 2 / 4 = PH / PV reduced to their centre tap, 8 = input loads read nothing
+#ifndef PCS_NRM_ABL
+#define PCS_NRM_ABL 0
+#endif
+template <typename T, int TX_, int RS_, int RB_>
+struct NrmG {
+  static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8, WI = 4 * GI;
+  static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX;
+  static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
+  static constexpr int NTAB = 288;  // a_v[0..29), a_h[32..61), E_v lo / hi, E_h lo / hi (7 x 8 each)
+  static_assert(NPH % NT == 0, "whole PH items per thread");
+  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TX + NTAB); }
+};
+template <typename T> struct NrmCfg;
+template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4>; };
+template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2>; };
+
+// compiler fences of the PV chunks: no LDS read or FMA moves across (bounds the registers held
+// by hoisted window reads) ...
+__device__ __forceinline__ void nrm_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// ... and the chunk's FMAs stay before the fence (not sunk below the later reads)
+template <typename T>
+__device__ __forceinline__ void nrm_pin(Q4<T>& a) {
+  asm volatile("" : "+v"(a.v[0]), "+v"(a.v[1]), "+v"(a.v[2]), "+v"(a.v[3]));
+}
+
+// 4 elements through a descriptor (16-B stores; an offset carrying kOOB is dropped)
+template <typename T>
+__device__ __forceinline__ void nrm_bstore(Rsrc r, uint32_t off, const Q4<T>& a) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  constexpr int VN = V16<T>::N;
+#pragma unroll
+  for (int h = 0; h < 4 / VN; ++h) {
+    u4 d;
+    __builtin_memcpy(&d, a.v + h * VN, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(off + 16 * h), 0, 0);
+  }
+}
+
+// tap d of a filter stored as h[0..k) with offset off (zero outside)
+__device__ __forceinline__ double nrm_tap(const double* h, int k, int off, int d) {
+  const int t = d + off;
+  return (t >= 0 && t < k) ? h[t] : 0.0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
+                                                                 int n2, int nstrips, int nseg, int seg_len,
+                                                                 int64_t ntasks, const T* __restrict__ ha_, int ka,
+                                                                 int offa, const T* __restrict__ hb_, int kb, int offb) {
+  using G = typename NrmCfg<T>::G;
+  constexpr int TX = G::TX, RS = G::RS, RB = G::RB, RING = G::RING, GX = G::GX, GI = G::GI, WI = G::WI, NT = G::NT,
+                NL = G::NL;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* stg = reinterpret_cast<T*>(smem_raw);  // RS x WI staged input rows
+  T* ring = stg + RS * WI;                  // RING x TX rows of the horizontal pass
+  T* tab = ring + RING * TX;                // NTAB
+  const int tid = threadIdx.x;
+  {
+    __shared__ double hs[32];  // the two filters in fp64
+    if (tid < 16) hs[tid] = tid < ka ? (double)ha_[tid] : 0.0;
+    else if (tid < 32) hs[tid] = tid - 16 < kb ? (double)hb_[tid - 16] : 0.0;
+    __syncthreads();
+    for (int e = tid; e < G::NTAB; e += NT) {
+      double v = 0.0;
+      if (e < 64) {
+        const int q = e & 31;
+        const double* h = e < 32 ? hs : hs + 16;
+        const int k = e < 32 ? ka : kb, off = e < 32 ? offa : offb;
+        if (q < 29)
+          for (int m = -7; m <= 7; ++m) v += nrm_tap(h, k, off, m) * nrm_tap(h, k, off, m + q - 14);
+      } else {
+        const int idx = e - 64, tb = idx / 56, r = idx - 56 * tb, j = r >> 3, c = r & 7;
+        const double* h = tb < 2 ? hs : hs + 16;
+        const int k = tb < 2 ? ka : kb, off = tb < 2 ? offa : offb;
+        if (c < 7) {
+          if ((tb & 1) == 0)  // rows / columns i = -7..-1 before the plane: E[j][c], j, c < 7
+            for (int i = -7; i < 0; ++i) v += nrm_tap(h, k, off, i - j) * nrm_tap(h, k, off, i - c);
+          else  // after it: j = n - 7 + jj, c = n - 7 + cc, i = n + ii
+            for (int ii = 0; ii < 7; ++ii) v += nrm_tap(h, k, off, 7 + ii - j) * nrm_tap(h, k, off, 7 + ii - c);
+        }
+      }
+      tab[e] = (T)v;
+    }
+    __syncthreads();
+  }
+  // the autocorrelation is symmetric: window tap q is a[|q - 14|], 15 registers per axis
+  T av[15], ah[15];
+#pragma unroll
+  for (int e = 0; e < 15; ++e) {
+    av[e] = tab[14 + e];
+    ah[e] = tab[32 + 14 + e];
+  }
+  const T* evl = tab + 64;
+  const T* evh = tab + 120;
+  const T* ehl = tab + 176;
+  const T* ehh = tab + 232;
+  int64_t t0, t_end, t_stride;
+  {  // XCD x owns a contiguous share of the task list; its blocks take consecutive tasks
+    const int64_t b = blockIdx.x, nb = gridDim.x, xcd = b % 8, k = b / 8, q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (xcd < r ? 1 : 0);
+    const int64_t before = xcd * q + (xcd < r ? xcd : r);
+    const int64_t lo = ntasks * before / nb, hi = ntasks * (before + nbx) / nb;
+    t0 = lo + k;
+    t_end = hi;
+    t_stride = nbx;
+  }
+  if (t0 >= t_end) return;
+  struct Cur {
+    int64_t t, plane;
+    int strip, a, b, s, ns;
+  };
+  auto task_at = [&](int64_t t) {
+    Cur c;
+    c.t = t;
+    const int64_t per_plane = (int64_t)nseg * nstrips;
+    c.plane = t / per_plane;
+    const int rem = (int)(t - c.plane * per_plane), seg = rem / nstrips;
+    c.strip = rem - seg * nstrips;
+    c.a = seg * seg_len;
+    c.b = min(n1, c.a + seg_len);
+    c.s = 0;
+    c.ns = (c.b - c.a + 28 + RS - 1) / RS;
+    return c;
+  };
+  Q4<T> q[NL];
+  // staged rows of step s: input rows a - 14 + s RS + rr, columns c0 - 16 + 4 gg (0 outside)
+  auto prefetch = [&](const Cur& c) {
+    const T* src = in + c.plane * (int64_t)n1 * n2;
+    const int kmax = c.b - c.a + 27;  // last staged row any output of [a, b) reads
+    const int gc0 = c.strip * TX - 16;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = min(l * NT + tid, G::NIN - 1);
+      const int rr = e / GI, gg = e - rr * GI;
+      const int k = c.s * RS + rr, gi = c.a - 14 + k, gc = gc0 + 4 * gg;
+      const bool ok = gi >= 0 && gi < n1 && k <= kmax && gc >= 0 && gc + 4 <= n2 && !(PCS_NRM_ABL & 8);
+      const Q4<T> v = ldq(src + (ok ? (int64_t)gi * n2 + gc : 0));
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
+    }
+  };
+  Cur cur = task_at(t0);
+  prefetch(cur);
+  const int vi = tid / GX, vg = tid - vi * GX;  // PV item: rows RB vi .. + RB - 1 of the step, group vg
+  for (;;) {
+    // the staged rows have landed; the previous step's RB row stores (4 / 8 dwordx4) may still
+    // be in flight (vector memory ops retire in order)
+    __builtin_amdgcn_s_waitcnt((G::NST & 15) | ((G::NST >> 4) << 14) | (7 << 4) | (15 << 8));
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int e = l * NT + tid;
+      if (e < G::NIN) stq(stg + 4 * e, q[l]);
+    }
+    Cur nxt = cur;
+    bool more = true;
+    if (cur.s + 1 < cur.ns) {
+      nxt.s = cur.s + 1;
+    } else {
+      more = cur.t + t_stride < t_end;
+      if (more) nxt = task_at(cur.t + t_stride);
+    }
+    prefetch(nxt);  // unconditional (the last step re-reads its own rows): the wait for these
+                    // loads at the next step then leaves this step's stores in flight
+    const int c0 = cur.strip * TX;
+    const int sb = (cur.s * RS) % RING;  // ring slot of the step's first staged row
+    lds_barrier();
+    // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q)
+#pragma unroll 1
+    for (int l = 0; l < G::NPH / NT; ++l) {
+      const int e = l * NT + tid, r = e / GX, g = e - r * GX;
+      const T* srow = stg + r * WI;
+      T acc[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        const Q4<T> v = ldsq(srow + 4 * (g + u));
+#pragma unroll
+        for (int ee = 0; ee < 4; ++ee)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int qq = 4 * u + ee - m - 2;
+            if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 2) || qq == 14)) acc[m] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
+          }
+      }
+      const int col = c0 + 4 * g;
+      if (col < 7 || col + 3 >= n2 - 7) {  // the edge terms of the first / last 7 columns
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int j = col + m;
+          if (j < 7) {
+            for (int c = 0; c < 7; ++c) acc[m] -= ehl[8 * j + c] * srow[16 + c];
+          } else if (j >= n2 - 7 && j < n2) {
+            const int jj = j - (n2 - 7), s0 = n2 - 7 - c0 + 16;
+            for (int c = 0; c < 7; ++c) acc[m] -= ehh[8 * jj + c] * srow[s0 + c];
+          }
+        }
+      }
+      int slot = sb + r;
+      slot = slot >= RING ? slot - RING : slot;
+      Q4<T> o;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) o.v[m] = acc[m];
+      stq(ring + slot * TX + 4 * g, o);
+    }
+    lds_barrier();
+    // ---- PV: out row i = a - 28 + s RS + r reads t rows i - 14 .. i + 14 (staged s RS + r - 28 ..)
+    {
+      const int r0 = RB * vi;
+      const int base = (cur.s * RS + r0 - 28 + RING) % RING;
+      Q4<T> acc[RB];
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[rr].v[m] = T(0);
+      // RB + 28 window rows in chunks of CH, the next chunk's reads in flight during this one's FMAs
+      constexpr int NV = RB + 28, CH = sizeof(T) == 4 ? 8 : 4, NCH = (NV + CH - 1) / CH;
+      const T* rcol = ring + 4 * vg;
+      Q4<T> wa[CH], wb[CH];
+      auto rd = [&](int c, Q4<T>(&w)[CH]) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          if (c * CH + j < NV) {
+            int slot = base + c * CH + j;
+            slot = slot >= RING ? slot - RING : slot;
+            w[j] = ldsq(rcol + slot * TX);
+          }
+        }
+      };
+      rd(0, wa);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) rd(c + 1, wb);
+        nrm_fence();
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int v = c * CH + j;
+          if (v < NV) {
+#pragma unroll
+            for (int rr = 0; rr < RB; ++rr) {
+              const int qq = v - rr;
+              if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 4) || qq == 14)) {
+                const T h = av[qq < 14 ? 14 - qq : qq - 14];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc[rr].v[m] += h * wa[j].v[m];
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) nrm_pin(acc[rr]);
+        nrm_fence();
+#pragma unroll
+        for (int j = 0; j < CH; ++j) wa[j] = wb[j];
+      }
+      const int gc = c0 + 4 * vg;
+      // every thread issues RB stores per step (rows outside [a, b) dropped by the range check),
+      // so the next step's wait for its staged rows leaves these stores in flight
+      const Rsrc dst = rsrc_of(out + cur.plane * (int64_t)n1 * n2, (uint32_t)((int64_t)n1 * n2 * sizeof(T)));
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr) {
+        const int i = cur.a - 28 + cur.s * RS + r0 + rr;
+        const bool live = i >= cur.a && i < cur.b && gc < n2;
+        if (live) {
+          if (i < 7 || i >= n1 - 7) {  // the edge terms of the first / last 7 rows
+            const bool top = i < 7;
+            const int jr = top ? i : i - (n1 - 7), row0 = top ? 0 : n1 - 7;
+            const T* e = top ? evl : evh;
+            for (int c = 0; c < 7; ++c) {
+              const Q4<T> w = ldsq(ring + ((row0 + c - cur.a + 14) % RING) * TX + 4 * vg);
+              const T ec = e[8 * jr + c];
+#pragma unroll
+              for (int m = 0; m < 4; ++m) acc[rr].v[m] -= ec * w.v[m];
+            }
+          }
+        }
+        nrm_bstore(dst, live && !(PCS_NRM_ABL & 1) ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB, acc[rr]);
+      }
+    }
+    if (!more) break;
+    cur = nxt;
+  }
+}
+
+template <typename T>
+static void nrm_attr() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep2d_nrm<T>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)NrmCfg<T>::G::lds_bytes());
+    (void)hipGetLastError();
+    done = true;
+  }
+}
+
+template <typename T>
+static int nrm_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    using G = typename NrmCfg<T>::G;
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    nrm_attr<T>();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_nrm<T>, G::NT, G::lds_bytes()) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+    (void)hipGetLastError();
+    slots = cus * nb;
+    const char* e = getenv("PCS_ATA_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
+  }
+  return slots;
+}
+
+// the two-pass kernel takes taps reaching <= 7 samples either side (any centred filter of
+// <= 15 taps) on planes of >= 16 x 16; PCS_ATA_KERNEL=4pass pins the four-pass kernel (diagnostics)
+static bool nrm_fits(int64_t n1, int64_t n2, int ka, int offa, int kb, int offb) {
+  const char* e = getenv("PCS_ATA_KERNEL");
+  if (e && strcmp(e, "4pass") == 0) return false;
+  return n1 >= 16 && n2 >= 16 && n2 % 4 == 0 && offa <= 7 && ka - 1 - offa <= 7 && offb <= 7 && kb - 1 - offb <= 7;
+}
+
+template <typename T>
+static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
+                   const void* hb, int kb, int offb, hipStream_t st) {
+  using G = typename NrmCfg<T>::G;
+  if (np == 0) return PCS_OK;
+  const int64_t nstrips = (n2 + G::TX - 1) / G::TX, pieces = np * nstrips;
+  const int64_t slots = nrm_slots<T>();
+  // row segments: the count minimising (waves of resident workgroups) x (rows per task + the
+  // 28-row prologue), segments of >= 64 rows
+  const int64_t max_seg = n1 / 64 > 1 ? n1 / 64 : 1;
+  int64_t nseg = 1, best = -1;
+  for (int64_t c = 1; c <= max_seg; ++c) {
+    const int64_t len = (n1 + c - 1) / c, waves = (pieces * c + slots - 1) / slots;
+    const int64_t cost = waves * (len + 28);
+    if (best < 0 || cost < best) {
+      best = cost;
+      nseg = c;
+    }
+  }
+  const int64_t seg_len = (n1 + nseg - 1) / nseg;
+  nseg = (n1 + seg_len - 1) / seg_len;
+  const int64_t ntasks = pieces * nseg;
+  const int64_t grid = ntasks < slots ? ntasks : slots;
+  nrm_attr<T>();
+  k_sep2d_nrm<T><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>((const T*)in, (T*)out, (int)n1, (int)n2,
+                                                                (int)nstrips, (int)nseg, (int)seg_len, ntasks,
+                                                                (const T*)ha, ka, offa, (const T*)hb, kb, offb);
+  return launch_status();
+}
+
 template <typename T>
 static int sep_ata(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
                    const void* hb, int kb, int offb, hipStream_t st) {
@@ -314,6 +688,8 @@ static int sep_ata(const void* in, void* out, int64_t np, int64_t n1, int64_t n2
       offa < 0 || offa >= ka || offb < 0 || offb >= kb || in == out)
     return PCS_EINVAL;
   if ((uintptr_t)in % 16 || (uintptr_t)out % 16) return PCS_EINVAL;
+  if (nrm_fits(n1, n2, ka, offa, kb, offb) && n1 * n2 * (int64_t)sizeof(T) < (1LL << 30))
+    return sep_nrm<T>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st);
   const int padb = ata_padb(kb, offb);
   if (padb < 0 || n2 % 4 != 0 || n1 >= (1LL << 30) || n2 >= (1LL << 30)) return PCS_EUNSUPPORTED;
   if (np == 0) return PCS_OK;

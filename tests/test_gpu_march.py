@@ -166,3 +166,47 @@ def test_c2_full_size_fused_vs_generic():
     assert rel(xf, xg) < 1e-5 and rel(zf, zg) < 1e-5
     for col in ('Relative Improvement (primal variable)', 'Relative Improvement (dual variable)'):
         np.testing.assert_allclose(df[col].to_numpy(float)[1:], dg[col].to_numpy(float)[1:], rtol=1e-3)
+
+
+SEP_CASES = [i for i, c in enumerate(CASES) if c[1] > 0]
+
+
+@pytest.mark.parametrize('case', SEP_CASES)
+def test_fourpass_march_vs_oracle(case, monkeypatch):
+    """The separable cases again with PCS_NMARCH=0: grad F = Conv^T (Conv x - y) as four
+    15-tap passes (pds_march.hpp) instead of N x - Conv^T y (pds_nmarch.hpp, the default
+    above) -- both kernels stay parity-green against the oracle."""
+    monkeypatch.setenv('PCS_NMARCH', '0')
+    shape, L, hname, gname, steps = CASES[case]
+    p = _problem(shape, L, hname, gname, steps, seed=case)
+    xr, zr, dr, lip = _oracle(p)
+    x, z, diag = _fused(p, lip)
+    assert rel(x, xr) < 5e-5, rel(x, xr)
+    assert rel(z, zr) < 5e-5, rel(z, zr)
+
+
+def test_c3_full_size_normal_vs_fourpass(monkeypatch):
+    """C3 exactly (BASELINE north_star: 4096^2 fp32, 15x15 Gaussian PSF, K = forward
+    Gradient, 0.05 * L21Norm), 12 iterations, through the normal-operator kernel (the bench's)
+    and the four-pass kernel: the two gradient factorisations agree to fp32 rounding (x and z
+    to 1e-5 relative), the same iteration count, diagnostics to 1e-3."""
+    import torch
+
+    import bench
+    out = {}
+    for nm in ('1', '0'):
+        monkeypatch.setenv('PCS_NMARCH', nm)
+        pds = bench.build_problem(4096, 4096, torch.float32, lipschitz='analytic')
+        pds.max_iter = pds.min_iter = NITER - 1
+        pds.accuracy_threshold = 0.0
+        est, _, diag = pds.iterate()
+        eng = pds._engine
+        assert eng is not None and pds.iter == NITER
+        assert (eng.args.cty is not None and eng.args.cty != 0) == (nm == '1')
+        out[nm] = (est['primal_variable'].cpu().numpy(), est['dual_variable'].cpu().numpy(), diag)
+    (xn, zn, dn), (xf, zf, df) = out['1'], out['0']
+    assert np.isfinite(xn).all() and np.abs(xn).max() > 0
+    assert rel(xn, xf) < 1e-5, rel(xn, xf)
+    assert rel(zn, zf) < 1e-5, rel(zn, zf)
+    for col in ('Relative Improvement (primal variable)', 'Relative Improvement (dual variable)'):
+        np.testing.assert_allclose(dn[col].to_numpy(float)[1:], df[col].to_numpy(float)[1:], rtol=1e-3)

@@ -188,3 +188,33 @@ def test_nmarch_tables_equal_dense_normal_operator(half):
                         v -= tab[64 + 24 * H + 8 * (k - (n - H)) + (8 - H) + (j - (n - H))]
                 M[j, k] = v
         np.testing.assert_allclose(M, N, atol=2e-8)
+
+
+@pytest.mark.parametrize('k,off', [(15, 7), (6, 2), (3, 0), (5, 1), (1, 0), (2, 1), (8, 0), (8, 7)])
+@pytest.mark.parametrize('n', [16, 17, 40])
+def test_sep2d_nrm_tables_equal_dense_normal_operator(k, off, n):
+    """The tables k_sep2d_nrm (csrc/sep_ata.hip) builds per workgroup: for taps reaching <= 7
+    samples either side, C^T C of a zero-boundary Convolve1D (out[j] = sum_t h[t] in[j + off - t])
+    is a[j - k] (a the taps' autocorrelation, c(d) = h[d + off]) minus the 7x7 blocks of the
+    terms outside the line at each end -- equal to the dense C^T C, planes down to 16 samples."""
+    rng = np.random.default_rng(k * 100 + off * 10 + n)
+    h = rng.standard_normal(k)
+    C = np.zeros((n, n))
+    for j in range(n):
+        for i in range(n):
+            if 0 <= j + off - i < k:
+                C[j, i] = h[j + off - i]
+
+    def c(d):
+        return h[d + off] if 0 <= d + off < k else 0.0
+    a = [sum(c(m) * c(m + e) for m in range(-7, 8)) for e in range(-14, 15)]
+    N = np.zeros((n, n))
+    for j in range(n):
+        for q in range(29):
+            if 0 <= j - 14 + q < n:
+                N[j, j - 14 + q] = a[q]
+    for j in range(7):
+        for cc in range(7):
+            N[j, cc] -= sum(c(i - j) * c(i - cc) for i in range(-7, 0))
+            N[n - 7 + j, n - 7 + cc] -= sum(c(7 + ii - j) * c(7 + ii - cc) for ii in range(7))
+    np.testing.assert_allclose(N, C.T @ C, atol=1e-12)

@@ -1,6 +1,6 @@
 """Time the in-plane normal operator C12^T C12 of the 3-D engine: one pcs_conv2d_sep_ata_planes
-launch against the two pcs_conv2d_sep_planes launches (forward, flipped) it replaces, on the C4
-(512^3 f32) and C5 (1024^3 f64) volumes.  HIP events, median of 10 after 3 warm-up launches."""
+launch (both of its kernels) against the two pcs_conv2d_sep_planes launches (forward, flipped) it
+replaces, on the C4 (512^3 f32) and C5 (1024^3 f64) volumes.  HIP events, median of 10 after 3 warm-up launches."""
 import os
 import sys
 import numpy as np
@@ -45,10 +45,14 @@ def main():
         def one():
             assert lib.pcs_conv2d_sep_ata_planes(code, L.ptr(x), L.ptr(t), n, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7,
                                                  st) == 0
-        t2, t1 = med_ms(two), med_ms(one)
-        d = (g - t).abs().max().item() / g.abs().max().item()
-        print(f'{os.environ.get("PCS_LIB_PATH", "default")} n={n} {dt}: two passes {t2:.3f} ms, ata {t1:.3f} ms, '
-              f'max rel diff {d:.2e}', flush=True)
+        t2 = med_ms(two)
+        for kern in ('2pass', '4pass'):  # k_sep2d_nrm (two 29-tap passes) / k_sep2d_ata (four 15-tap)
+            os.environ['PCS_ATA_KERNEL'] = kern
+            t1 = med_ms(one)
+            d = (g - t).abs().max().item() / g.abs().max().item()
+            print(f'{os.environ.get("PCS_LIB_PATH", "default")} n={n} {dt}: two passes {t2:.3f} ms, ata[{kern}] '
+                  f'{t1:.3f} ms, max rel diff {d:.2e}', flush=True)
+        os.environ.pop('PCS_ATA_KERNEL')
         del x, t, g
 
 
