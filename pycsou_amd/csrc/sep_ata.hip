@@ -328,18 +328,29 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_ABL
 #define PCS_NRM_ABL 0
 #endif
-template <typename T, int TX_, int RS_, int RB_>
+template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
+  static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
   static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8, WI = 4 * GI;
-  static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX;
+  static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
   static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
   static constexpr int NTAB = 288;  // a_v[0..29), a_h[32..61), E_v lo / hi, E_h lo / hi (7 x 8 each)
   static_assert(NPH % NT == 0, "whole PH items per thread");
   static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TX + NTAB); }
 };
 template <typename T> struct NrmCfg;
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2>; };
+#ifndef PCS_NRM_CFG
+#define PCS_NRM_CFG 0
+#endif
+#if PCS_NRM_CFG == 0
+template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 1>; };
+template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 1>; };
+#else  // diagnostics: 128 threads, RB 8 / 4 and 16 / 8-output PH items -- fewer LDS bytes per
+       // output (38 against 77 B in fp32) but half the waves: 0.69 against 0.57 ms (512^3 fp32),
+       // 9.4 against 7.8 ms (1024^3 fp64), profiles/r2_nrm_ablation.txt
+template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 8, 4>; };
+template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 4, 2>; };
+#endif
 
 // compiler fences of the PV chunks: no LDS read or FMA moves across (bounds the registers held
 // by hoisted window reads) ...
@@ -494,42 +505,50 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
     const int c0 = cur.strip * TX;
     const int sb = (cur.s * RS) % RING;  // ring slot of the step's first staged row
     lds_barrier();
-    // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q)
+    // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q);
+    // an item is 4 PQ consecutive outputs of one row (PQ + 8 window reads)
 #pragma unroll 1
     for (int l = 0; l < G::NPH / NT; ++l) {
-      const int e = l * NT + tid, r = e / GX, g = e - r * GX;
+      constexpr int PQ = G::PQ, GQ = GX / PQ;
+      const int e = l * NT + tid, r = e / GQ, g = PQ * (e - r * GQ);
       const T* srow = stg + r * WI;
-      T acc[4] = {T(0), T(0), T(0), T(0)};
+      T acc[4 * PQ];
 #pragma unroll
-      for (int u = 0; u < 9; ++u) {
+      for (int o = 0; o < 4 * PQ; ++o) acc[o] = T(0);
+#pragma unroll
+      for (int u = 0; u < PQ + 8; ++u) {
         const Q4<T> v = ldsq(srow + 4 * (g + u));
 #pragma unroll
         for (int ee = 0; ee < 4; ++ee)
 #pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const int qq = 4 * u + ee - m - 2;
-            if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 2) || qq == 14)) acc[m] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
+          for (int o = 0; o < 4 * PQ; ++o) {
+            const int qq = 4 * u + ee - o - 2;
+            if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 2) || qq == 14))
+              acc[o] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
           }
       }
       const int col = c0 + 4 * g;
-      if (col < 7 || col + 3 >= n2 - 7) {  // the edge terms of the first / last 7 columns
+      if (col < 7 || col + 4 * PQ - 1 >= n2 - 7) {  // the edge terms of the first / last 7 columns
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int j = col + m;
+        for (int o = 0; o < 4 * PQ; ++o) {
+          const int j = col + o;
           if (j < 7) {
-            for (int c = 0; c < 7; ++c) acc[m] -= ehl[8 * j + c] * srow[16 + c];
+            for (int c = 0; c < 7; ++c) acc[o] -= ehl[8 * j + c] * srow[16 + c];
           } else if (j >= n2 - 7 && j < n2) {
             const int jj = j - (n2 - 7), s0 = n2 - 7 - c0 + 16;
-            for (int c = 0; c < 7; ++c) acc[m] -= ehh[8 * jj + c] * srow[s0 + c];
+            for (int c = 0; c < 7; ++c) acc[o] -= ehh[8 * jj + c] * srow[s0 + c];
           }
         }
       }
       int slot = sb + r;
       slot = slot >= RING ? slot - RING : slot;
-      Q4<T> o;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) o.v[m] = acc[m];
-      stq(ring + slot * TX + 4 * g, o);
+      for (int p = 0; p < PQ; ++p) {
+        Q4<T> o;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o.v[m] = acc[4 * p + m];
+        stq(ring + slot * TX + 4 * (g + p), o);
+      }
     }
     lds_barrier();
     // ---- PV: out row i = a - 28 + s RS + r reads t rows i - 14 .. i + 14 (staged s RS + r - 28 ..)

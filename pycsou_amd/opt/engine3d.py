@@ -167,14 +167,16 @@ class PDS3DEngine:
                 esz = torch.empty(0, dtype=dtype).element_size()
                 self.sep2 = (sorted(c[0] for c in self.inplane) == [1, 2] and all(c[3] <= 15 for c in self.inplane)
                              and (plane * esz) % 16 == 0)
-                # opt-in (PCS_3D_ATA=1): the in-plane normal operator in one launch
-                # (pcs_conv2d_sep_ata_planes).  The axis-0 pass commutes with the in-plane ones, so
+                # the in-plane normal operator in one launch (pcs_conv2d_sep_ata_planes: two
+                # 29-tap passes).  The axis-0 pass commutes with the in-plane ones, so
                 # g = C0^T (C0 (C12^T C12 x) - C12^T y) with C12^T y formed here once: two
-                # sub-volume passes per iteration instead of three (14 words/voxel, not 16), but
-                # the four-pass kernel is LDS/latency-bound at one fp64 workgroup per CU and
-                # measured slower than the two passes it replaces
+                # sub-volume passes per iteration instead of three (15 words/voxel, not 17).
+                # Default for fp32 (C4: 568-571 against 541-546 it/s); fp64 measured even (C5
+                # 36.2 it/s both ways: the in-plane work is FMA / LDS-bound, not HBM-bound), so
+                # it keeps the three-pass chain.  PCS_3D_ATA=0/1 overrides
                 self.ata = False
-                if self.sep2 and os.environ.get('PCS_3D_ATA', '0') == '1':
+                ata_default = '1' if dtype == torch.float32 else '0'
+                if self.sep2 and os.environ.get('PCS_3D_ATA', ata_default) == '1':
                     (ha, ka, oa), (hb, kb, ob) = self._inplane_ab(False)
                     rc = self.lib.pcs_conv2d_sep_ata_planes(L.dtcode(self.T[0]), L.ptr(self.T[0]), L.ptr(self.T[1]),
                                                             0, n1, n2, L.ptr(ha), ka, oa, L.ptr(hb), kb, ob,

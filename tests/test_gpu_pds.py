@@ -230,10 +230,10 @@ def test_pds3d_fused_matches_reference(name, dtype):
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 def test_pds3d_ata_opt_in_matches_reference(monkeypatch, dtype):
-    """The opt-in two-pass gradient (PCS_3D_ATA=1: pcs_conv2d_sep_ata_planes + the axis-0 pass
-    against C12^T y).  The golden volume's last axis (22) is not a multiple of 4, which the
-    four-pass kernel needs: there the engine keeps the three-pass chain (same trajectory); on a
-    24 x 20 x 24 volume the two-pass gradient runs and matches the oracle."""
+    """The two-pass gradient (PCS_3D_ATA=1, the fp32 default: pcs_conv2d_sep_ata_planes + the
+    axis-0 pass against C12^T y).  The golden volume's last axis (22) is not a multiple of 4,
+    which the in-plane kernels need: there the engine keeps the three-pass chain (same
+    trajectory); on a 24 x 20 x 24 volume the two-pass gradient runs and matches the oracle."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     monkeypatch.setenv('PCS_3D_ATA', '1')
     c = pds_case('deconv3d_l21_fwd_24_sep15')
@@ -372,6 +372,29 @@ def test_pds3d_ragged_tiles_vs_oracle(shape, dtype):
     est, _, diag = pds.iterate()
     assert pds.iter == 8
     x_ref, z_ref, d_ref = oracle_pds(c)
+    tol = 1e-10 if dtype == np.float64 else 5e-5
+    assert rel(est['primal_variable'], x_ref) < tol
+    assert rel(est['dual_variable'], z_ref) < tol
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('ata', ['', '0'])
+def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
+    """Which 3-D gradient runs: by default the two-pass one (C12^T C12, then the axis-0 pass) for
+    fp32 and the three-pass chain for fp64; PCS_3D_ATA=0 pins the three-pass chain.  Either way
+    the iterates match the oracle."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    if ata:
+        monkeypatch.setenv('PCS_3D_ATA', ata)
+    else:
+        monkeypatch.delenv('PCS_3D_ATA', raising=False)
+    c = _vol_problem(24, dtype, seed=7, niter=12, shape=(20, 24, 32))
+    pds = build(c, dtype, engine='fused')
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    est, _, _ = pds.iterate()
+    assert isinstance(pds._engine, PDS3DEngine)
+    assert pds._engine.ata == (dtype == np.float32 and not ata)
+    x_ref, z_ref, _ = oracle_pds(c)
     tol = 1e-10 if dtype == np.float64 else 5e-5
     assert rel(est['primal_variable'], x_ref) < tol
     assert rel(est['dual_variable'], z_ref) < tol

@@ -8,4 +8,6 @@ tail -3 gpurun_out/${1:-ck}/gpu_tests.txt
 timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 > gpurun_out/${1:-ck}/bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/${1:-ck}/bench.log; exit 2; }
 tail -1 gpurun_out/${1:-ck}/bench.log
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${1:-ck}/prof -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/${1:-ck}/prof.log 2>&1 || { echo PROF_FAILED; tail -20 gpurun_out/${1:-ck}/prof.log; exit 3; }
+# the per-dispatch trace is tens of MB (gpurun_out/ comes back only under 64 MiB): keep the stats
+find gpurun_out/${1:-ck}/prof \( -name '*kernel_trace.csv' -o -name '*agent_info.csv' \) -delete
 echo ALL_OK
