@@ -566,21 +566,21 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
       // RB + 28 window rows in chunks of CH, the next chunk's reads in flight during this one's FMAs
       constexpr int NV = RB + 28, CH = sizeof(T) == 4 ? 8 : 4, NCH = (NV + CH - 1) / CH;
       const T* rcol = ring + 4 * vg;
-      Q4<T> wa[CH], wb[CH];
-      auto rd = [&](int c, Q4<T>(&w)[CH]) {
+      Q4<T> w[2][CH];  // chunk c in w[c & 1] (static after unrolling: no register copies)
+      auto rd = [&](int c, Q4<T>(&wc)[CH]) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
           if (c * CH + j < NV) {
             int slot = base + c * CH + j;
             slot = slot >= RING ? slot - RING : slot;
-            w[j] = ldsq(rcol + slot * TX);
+            wc[j] = ldsq(rcol + slot * TX);
           }
         }
       };
-      rd(0, wa);
+      rd(0, w[0]);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) rd(c + 1, wb);
+        if (c + 1 < NCH) rd(c + 1, w[(c + 1) & 1]);
         nrm_fence();
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
               if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 4) || qq == 14)) {
                 const T h = av[qq < 14 ? 14 - qq : qq - 14];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) acc[rr].v[m] += h * wa[j].v[m];
+                for (int m = 0; m < 4; ++m) acc[rr].v[m] += h * w[c & 1][j].v[m];
               }
             }
           }
@@ -600,8 +600,6 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
 #pragma unroll
         for (int rr = 0; rr < RB; ++rr) nrm_pin(acc[rr]);
         nrm_fence();
-#pragma unroll
-        for (int j = 0; j < CH; ++j) wa[j] = wb[j];
       }
       const int gc = c0 + 4 * vg;
       // every thread issues RB stores per step (rows outside [a, b) dropped by the range check),
