@@ -241,7 +241,10 @@ def volume_bench(n, dtype, K, W, world, rank):
                       world=world, chunk=2)
     del pds, spec
     torch.cuda.empty_cache()
-    total = W + K + 4
+    # iteration budget of the device loop control: the warmup, the timed iterations and the
+    # multi-GPU schedule trial (up to 8 eager iterations inside the first advance), with slack, so
+    # no timed launch finds the loop already stopped
+    total = W + K + 24
     eng.init_loop(total, total, -1.0)
     eng.advance(W)
     torch.cuda.synchronize()
@@ -272,7 +275,8 @@ def volume_bench(n, dtype, K, W, world, rank):
            'iteration_frac_of_hbm_peak_per_gpu': round(alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
            'alg_bytes_per_iter': alg, 'halo_bytes_per_side_per_iter': halo,
            'banded_overlap': bool(getattr(eng, 'banded', False) and eng.overlap),
-           'banded_order': getattr(eng, 'order', None) if world > 1 else None,
+           'banded_order': ((eng.order if eng.overlap else 'serial') if getattr(eng, 'banded', False) else None)
+                           if world > 1 else None,
            'order_trial_ms': getattr(eng, 'tune_ms', None),
            'setup_s': round(t1 - t0, 1)}
     del eng
@@ -442,6 +446,10 @@ def slab_bench(n, dtype, K, W, world):
     total = W + K + 4
     eng.init_loop(total, total, -1.0)
     spin_up(eng, min(K, 50))
+    if world > 1:  # the one-off serial / overlapped schedule trial runs here, never in the timed region
+        eng.init_loop(total, total, -1.0)
+        eng.advance(8)
+        torch.cuda.synchronize()
     eng.init_loop(total, total, -1.0)  # fixed count: the loop never stops early
     eng.advance(W)
     torch.cuda.synchronize()
@@ -607,7 +615,7 @@ def volume_leg(args, out, key, edge, dtype_v, steps, world, rank):
     timer.start()
     try:
         K = max(2, steps + steps % 2)
-        vres = volume_bench(edge, dtype_v, K, 6, world, rank)  # warmup also picks the banded order
+        vres = volume_bench(edge, dtype_v, K, 8, world, rank)  # warmup also picks the schedule
     except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
         vres = {'error': f'{type(e).__name__}: {e}'[:300]}
         print(f'bench: volume leg failed: {vres["error"]}', file=sys.stderr)

@@ -202,8 +202,8 @@ class PDS3DEngine:
         # band; the exchange overlaps the interior update only).  Same arithmetic either way.
         self.order = os.environ.get('PCS_3D_ORDER', 'split')
         # which order wins depends on the link speed (the halo bytes vs the overlap window):
-        # with a real transport the first advance() of >= 5 iterations times both and keeps
-        # the faster (max over ranks), unless PCS_3D_ORDER fixes it
+        # with a real transport the first advance() of >= 7 iterations times both and the serial
+        # schedule and keeps the fastest (max over ranks), unless PCS_3D_ORDER fixes it
         self._tuned = 'PCS_3D_ORDER' in os.environ or not getattr(comm, 'tunable', False)
         if fk == L.PCS_F_GRADBUF and self.fused0 and self.sep2 and not self.ata and self.rows > 2 * self.band:
             # g in a buffer of its own: the banded order writes g on the boundary planes while the
@@ -524,7 +524,7 @@ class PDS3DEngine:
 
     def advance(self, k):
         """Enqueue k iterations (k a multiple of the chunk when graphs are used)."""
-        if self.use_graph and self.world > 1 and not self._tuned and self.banded and self.overlap and k >= 5:
+        if self.use_graph and self.world > 1 and not self._tuned and self.banded and self.overlap and k >= 7:
             self._autotune()  # eager, before the capture; then back to parity 0 for the graph
             if self._p == 1:
                 self.iteration(1)
@@ -534,7 +534,7 @@ class PDS3DEngine:
             for _ in range(k // self.chunk):
                 self.graph.replay()
             return
-        if not self._tuned and self.banded and self.overlap and k >= 5:
+        if not self._tuned and self.banded and self.overlap and k >= 7:
             k -= self._autotune()
         for _ in range(k):
             self.iteration(self._p)
@@ -542,13 +542,18 @@ class PDS3DEngine:
         self._drain()
 
     def _autotune(self):
-        """Time 2 iterations in each banded order (after one untimed) and keep the faster;
-        every rank takes the same decision (max over ranks).  Returns the iterations used."""
+        """Time 2 iterations in each banded order and in the serial schedule (compute, then the
+        blocking all-gather and exchange) after one untimed, and keep the fastest; every rank takes
+        the same decision (max over ranks).  The three schedules compute bitwise the same iterates.
+        Returns the iterations used."""
         self.iteration(self._p)
         self._p ^= 1
+        cands = ('split', 'fullg', 'serial')
         times = []
-        for order in ('split', 'fullg'):
-            self.order = order
+        for cand in cands:
+            self.overlap = cand != 'serial'
+            if self.overlap:
+                self.order = cand
             self._drain()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -561,14 +566,17 @@ class PDS3DEngine:
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))
         dev = self.sums.device
-        mine = torch.tensor(times + [0.0, 0.0], dtype=torch.float64, device=dev)
+        mine = torch.tensor(times + [0.0], dtype=torch.float64, device=dev)
         allt = torch.zeros(4 * self.world, dtype=torch.float64, device=dev)
         self.comm.allgather(mine, allt)
-        worst = allt.view(self.world, 4).max(dim=0).values
-        self.order = 'split' if float(worst[0]) <= float(worst[1]) else 'fullg'
-        self.tune_ms = [float(worst[0]) / 2, float(worst[1]) / 2]
+        worst = allt.view(self.world, 4).max(dim=0).values[:3]
+        best = int(torch.argmin(worst).item())
+        self.overlap = cands[best] != 'serial'
+        if self.overlap:
+            self.order = cands[best]
+        self.tune_ms = {c: float(worst[i]) / 2 for i, c in enumerate(cands)}
         self._tuned = True
-        return 5
+        return 7
 
     def iterations(self):
         return int(self.ctrl.view(torch.int32)[0].item())
