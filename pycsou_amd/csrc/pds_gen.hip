@@ -26,8 +26,11 @@ namespace pcs {
 
 enum { KK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED gradients, or the Laplacian
 
+#ifndef PCS_GEN_TR
+#define PCS_GEN_TR 32
+#endif
 struct GenG {
-  static constexpr int TR = 32, TC = 64, NT = 256;
+  static constexpr int TR = PCS_GEN_TR, TC = 64, NT = 256;
   static constexpr int CW = TC + 8, CG = CW / 4;  // LDS columns [c0 - 4, c0 + TC + 4)
   static constexpr int ZR = TR + 8, UR = TR + 4;  // Z rows [r0 - 4, r0 + TR + 4), U rows [r0 - 2, r0 + TR + 2)
   static constexpr int NZI = ZR * CG, NUI = UR * CG, NOI = TR * (TC / 4);
