@@ -26,6 +26,17 @@ namespace pcs {
 
 enum { KK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED gradients, or the Laplacian
 
+// phase barriers: LDS-only (s_waitcnt lgkmcnt(0) + s_barrier) by default -- no wave reads global
+// data another wave of the launch wrote, so the x' stores of the U phase need not have landed
+// before the Z phase (__syncthreads' release fence would wait for them); PCS_GEN_LDSBAR=0 restores it
+#ifndef PCS_GEN_LDSBAR
+#define PCS_GEN_LDSBAR 1
+#endif
+#if PCS_GEN_LDSBAR
+#define PCS_GEN_BARRIER() lds_barrier()
+#else
+#define PCS_GEN_BARRIER() __syncthreads()
+#endif
 #ifndef PCS_GEN_TR
 #define PCS_GEN_TR 32
 #endif
@@ -177,7 +188,7 @@ __device__ __forceinline__ void gen_tile(const T* __restrict__ x, T* __restrict_
         if (e < G::NZI) st4(Z + d * ZS + 4 * e, zr[d][k]);  // row rr, group g at rr * CW + 4 g = 4 e
       }
   }
-  __syncthreads();
+  PCS_GEN_BARRIER();
   // ---- U items: x_t, u on rows [r0 - 2, r0 + TR + 2) x columns [c0 - 2, c0 + TC + 2); x' on the tile
 #pragma unroll
   for (int k = 0; k < G::KU; ++k) {
@@ -222,7 +233,7 @@ __device__ __forceinline__ void gen_tile(const T* __restrict__ x, T* __restrict_
       }
     }
   }
-  __syncthreads();
+  PCS_GEN_BARRIER();
   // ---- z' on the tile
 #pragma unroll
   for (int k = 0; k < G::KO; ++k) {
