@@ -328,6 +328,9 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_ABL
 #define PCS_NRM_ABL 0
 #endif
+#ifndef PCS_NRM_CH  // PV window rows per pipelined chunk (0: 4); diagnostics
+#define PCS_NRM_CH 0
+#endif
 template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
   static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
@@ -564,7 +567,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[rr].v[m] = T(0);
       // RB + 28 window rows in chunks of CH, the next chunk's reads in flight during this one's FMAs
-      constexpr int NV = RB + 28, CH = sizeof(T) == 4 ? 8 : 4, NCH = (NV + CH - 1) / CH;
+      // 4-row chunks: 0.543 against 0.565-0.573 ms for 8 (512^3 fp32, profiles/r2_nrm_ablation.txt)
+      constexpr int NV = RB + 28, CH = PCS_NRM_CH > 0 ? PCS_NRM_CH : 4, NCH = (NV + CH - 1) / CH;
       const T* rcol = ring + 4 * vg;
       Q4<T> w[2][CH];  // chunk c in w[c & 1] (static after unrolling: no register copies)
       auto rd = [&](int c, Q4<T>(&wc)[CH]) {
