@@ -328,6 +328,9 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_ABL
 #define PCS_NRM_ABL 0
 #endif
+#ifndef PCS_NRM_PHU  // PH items unrolled per loop trip; diagnostics
+#define PCS_NRM_PHU 1
+#endif
 #ifndef PCS_NRM_CH  // PV window rows per pipelined chunk (0: 4); diagnostics
 #define PCS_NRM_CH 0
 #endif
@@ -390,7 +393,7 @@ __device__ __forceinline__ double nrm_tap(const double* h, int k, int off, int d
 }
 
 template <typename T>
-__global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
+__global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
                                                                  int n2, int nstrips, int nseg, int seg_len,
                                                                  int64_t ntasks, const T* __restrict__ ha_, int ka,
                                                                  int offa, const T* __restrict__ hb_, int kb, int offb) {
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT) void k_sep2d_nrm(const T* __restr
     lds_barrier();
     // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q);
     // an item is 4 PQ consecutive outputs of one row (PQ + 8 window reads)
-#pragma unroll 1
+#pragma unroll PCS_NRM_PHU
     for (int l = 0; l < G::NPH / NT; ++l) {
       constexpr int PQ = G::PQ, GQ = GX / PQ;
       const int e = l * NT + tid, r = e / GQ, g = PQ * (e - r * GQ);
