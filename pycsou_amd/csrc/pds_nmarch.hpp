@@ -66,6 +66,13 @@ __device__ __forceinline__ float lds1(const float* p) {
   return *(lds_f1)(p);
 }
 
+// wave priority 3 while a step's loads issue (s_setprio), 0 for its LDS / VALU phases: the loads
+// of every wave go out ahead of the other waves' FMAs -- 113.1-113.6 against 115.9-116.5 us
+// back to back (4 alternating reps, tools/march_ablate.py); PCS_NM_PRIO=0 drops it
+#ifndef PCS_NM_PRIO
+#define PCS_NM_PRIO 1
+#endif
+
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima)
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -458,11 +465,17 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     asm volatile("" : "+v"(wz));
     Wq = W + wz;
     // this step's z tiles (LDS-DMA) and b, the next step's x rows (registers, landed after P6)
+#if PCS_NM_PRIO
+    __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
+#endif
     load_z(a, 0);
     const uint32_t rb = vb.row_off(a + 1 + ui);
     bv = bload4(vb.r, rb + co_u);
     b5 = bload4(vb.r, rb + co_b5).v[0];
     load_xn(xnx, a + 2 * H + 1 + TS);
+#if PCS_NM_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     ph(a + 2 * H + 1 + ui);
     vm_wait<KXN + 2>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
