@@ -331,6 +331,9 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_PHU  // PH items unrolled per loop trip; diagnostics
 #define PCS_NRM_PHU 1
 #endif
+#ifndef PCS_NRM_PRIO  // wave priority 3 while the next step's loads issue; diagnostics
+#define PCS_NRM_PRIO 0
+#endif
 #ifndef PCS_NRM_CH  // PV window rows per pipelined chunk (0: 4); diagnostics
 #define PCS_NRM_CH 0
 #endif
@@ -509,8 +512,14 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       more = cur.t + t_stride < t_end;
       if (more) nxt = task_at(cur.t + t_stride);
     }
+#if PCS_NRM_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     prefetch(nxt);  // unconditional (the last step re-reads its own rows): the wait for these
                     // loads at the next step then leaves this step's stores in flight
+#if PCS_NRM_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     const int c0 = cur.strip * TX;
     const int sb = (cur.s * RS) % RING;  // ring slot of the step's first staged row
     lds_barrier();
