@@ -19,6 +19,12 @@
 
 namespace pcs {
 
+// wave priority 3 while a step's loads issue (as pds_nmarch.hpp): C2 29.8-30.1 against
+// 30.2-30.4 us per iteration (3 alternating reps, tools/c2_ab.sh); PCS_PT_PRIO=0 drops it
+#ifndef PCS_PT_PRIO
+#define PCS_PT_PRIO 1
+#endif
+
 struct PtGeom {
   static constexpr int TW = 64, TS = 16, UROWS = TS + 1, WG = TW + 4, GG = WG / 4;
   static constexpr int NZ0 = UROWS * GG, NZ1 = UROWS * (GG + 1);
@@ -216,10 +222,22 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
     const int fl = launder(flags);
     lds_barrier();  // previous P6 done with Z, U rows
     land_z();
+#if PCS_PT_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     if (k + 1 < nsteps) loads_z(a + TS);  // next step's z flies during this step's P45 and P6
+#if PCS_PT_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     lds_barrier();
     p45(a, fl, ub);
+#if PCS_PT_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     if (k + 1 < nsteps) loads_x(a + TS);  // next step's x, y|g during this step's P6
+#if PCS_PT_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     lds_barrier();
     p6(a, fl, ub);
     ub = ub == 0 ? 16 : ub - 1;
