@@ -18,6 +18,10 @@
 // outside the image pushed past the range: no branches, no selects.
 #include "pds_march.hpp"
 
+#ifndef PCS_3D_PRIO  // wave priority 3 while the next plane's loads issue; diagnostics
+#define PCS_3D_PRIO 0
+#endif
+
 namespace pcs {
 
 template <typename T>
@@ -208,7 +212,13 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
     G4<T> gv4;
     if constexpr (FK != PCS_F_NULL) gv4 = gr;
     land(slot);
+#if PCS_3D_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     if (p < p_end) prefetch(p + 1);
+#if PCS_3D_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     lds_barrier();
     const int fl = launder(flags);
     // ---- U items: x_t, u on rows [r1, r1 + T1], cols [c2, c2 + WG) of plane p; x' on own cells
