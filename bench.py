@@ -78,7 +78,7 @@ def aniso_psf(size=15, su=3.0, sv=1.2, angle=np.pi / 6):
     return h / h.sum()
 
 
-def build_problem(n0, n1, dtype, seed=0, psf=None, lipschitz='lanczos'):
+def build_problem(n0, n1, dtype, seed=0, psf=None, lipschitz='lanczos', kind='forward'):
     """The C3 problem through the public API (pycsou scripts look exactly like this).
     lipschitz='lanczos': K.compute_lipschitz_cst() / C.compute_lipschitz_cst() as a reference
     script does (device Lanczos, untimed setup); 'analytic': the closed forms (||grad_fwd|| from
@@ -91,7 +91,7 @@ def build_problem(n0, n1, dtype, seed=0, psf=None, lipschitz='lanczos'):
     N = n0 * n1
     xs = torch.as_tensor(phantom((n0, n1), 64, seed).ravel()).to('cuda', dtype)
     C = Convolve2D(size=N, filter=gaussian_psf(15, 2.0) if psf is None else psf, shape=(n0, n1))
-    K = Gradient(shape=(n0, n1), kind='forward')
+    K = Gradient(shape=(n0, n1), kind=kind)  # kind='centered': the reference's default Gradient(shape)
     if lipschitz == 'lanczos':
         C.compute_lipschitz_cst()
         K.compute_lipschitz_cst()
@@ -346,7 +346,9 @@ def leg_c2(args, dtype, K, W):
     """C2 (BASELINE configs[1]) 2048^2 fp32 TV denoising: it/s and the step kernel against the
     HBM roofline (7 N words per iteration)."""
     n = 2048
+    t0 = time.perf_counter()
     pds = build_denoise(n, dtype, lipschitz=args.lipschitz)
+    setup = time.perf_counter() - t0  # problem build incl. compute_lipschitz_cst (device Lanczos)
     r = fused_2d(pds, dtype, K, W)
     del pds
     elem = 4 if dtype == torch.float32 else 8
@@ -355,7 +357,7 @@ def leg_c2(args, dtype, K, W):
     return {'workload': f'C2 TV denoising {n}x{n} {args.dtype}, Gradient(kind=forward), 0.1*L21Norm, '
                         f'PDS fused step (pcs_pds2d_step, row-marching pointwise-F kernel)',
             'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
-            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg,
+            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg, 'setup_s': round(setup, 2),
             'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             'roofline': {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_pt<DENOISE,L21>)', 'kernel_ms': round(km, 5),
                          'achieved': round(alg / (km * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -364,7 +366,9 @@ def leg_c2(args, dtype, K, W):
 
 def _leg_stencil(args, dtype, K, W, kind):
     n = 2048
+    t0 = time.perf_counter()
     pds = build_denoise_k(n, dtype, kind, lipschitz=args.lipschitz)
+    setup = time.perf_counter() - t0
     r = fused_2d(pds, dtype, K, W)
     del pds
     elem = 4 if dtype == torch.float32 else 8
@@ -373,11 +377,11 @@ def _leg_stencil(args, dtype, K, W, kind):
     km = r['kernels_ms']['step']
     kdesc = 'Laplacian(edge=True), 0.1*L1Norm' if kind == 'lap' else 'Gradient(kind=centered, edge=True), 0.1*L21Norm'
     return {'workload': f'2-D denoising {n}x{n} {args.dtype}, K = {kdesc}, PDS fused general-stencil step '
-                        f'(pcs_pds2d_stencil_step, 32x64 tiles), iterations launched back to back from C',
+                        f'(row-marching k_pds2d_smarch through pcs_pds2d_step), iterations launched back to back from C',
             'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
-            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg,
+            'steps': K, 'warmup': W, 'alg_bytes_per_iter': alg, 'setup_s': round(setup, 2),
             'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            'roofline': {'bound': 'hbm', 'kernel': f'pcs_pds2d_stencil_step (k_pds2d_gen<float,{kind}>)',
+            'roofline': {'bound': 'hbm', 'kernel': f'pcs_pds2d_step (k_pds2d_smarch<{kind}, DENOISE>)',
                          'kernel_ms': round(km, 5), 'achieved': round(alg / (km * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
@@ -401,7 +405,9 @@ def leg_c3_nonsep(args, dtype, K, W):
     with grad F read from g (pcs_pds2d_step, GRADBUF); the three launches per iteration are
     replayed from a captured hipGraph."""
     n = args.size
+    t0 = time.perf_counter()
     pds = build_problem(n, n, dtype, psf=aniso_psf(), lipschitz=args.lipschitz)
+    setup = time.perf_counter() - t0
     r = fused_2d(pds, dtype, K, W)
     del pds
     elem = 4 if dtype == torch.float32 else 8
@@ -415,7 +421,7 @@ def leg_c3_nonsep(args, dtype, K, W):
                         f'conv r = h*x - y, g = h^T r (pcs_conv2d_planned x2) + fused update (GRADBUF), hipGraph-replayed',
             'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
             'steps': K, 'warmup': W, 'kernels_ms': {k: round(v, 5) for k, v in km.items()},
-            'alg_bytes_per_iter': alg,
+            'alg_bytes_per_iter': alg, 'setup_s': round(setup, 2),
             'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             'roofline': {'bound': 'fp32-vector', 'kernel': 'pcs_conv2d_planned (k_corr2d<float,15>)',
                          'kernel_ms': round(conv_ms, 5), 'achieved': round(conv_flop / (conv_ms * 1e-3) / 1e12, 2),
@@ -426,6 +432,42 @@ def leg_c3_nonsep(args, dtype, K, W):
                                 'kernel_ms': round(km['step'], 5),
                                 'achieved': round(alg / (km['step'] * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
                                 'unit': 'GB/s', 'frac': round(alg / (km['step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def leg_c3_cen(args, dtype, K, W):
+    """The C3 problem with the reference's DEFAULT K = Gradient(shape) (kind='centered', edge=True,
+    pycsou/linop/diff.py:777-778): grad F = N x - Conv^T y with N x = Conv^T Conv x by the in-plane
+    normal-operator kernel (two 29-tap passes, k_sep2d_nrm) into a buffer, then the general-stencil
+    row-marching step (k_pds2d_smarch, SEPCONV: reads x, N x, Conv^T y, z; writes x', z') -- two
+    launches per iteration, back to back from C."""
+    n = args.size
+    t0 = time.perf_counter()
+    pds = build_problem(n, n, dtype, lipschitz=args.lipschitz, kind='centered')
+    spec = pds._fused_spec()
+    setup = time.perf_counter() - t0
+    r = fused_2d(pds, dtype, K, W)
+    del pds
+    elem = 4 if dtype == torch.float32 else 8
+    N = n * n
+    alg = 7 * N * elem
+    km = r['kernels_ms']
+    upd = km['step'] - km.get('conv_nx', 0.0)
+    step_bytes = 8 * N * elem  # the update kernel's own traffic: x, N x, Conv^T y, z (2) in; x', z' (2) out
+    return {'workload': f'C3 TV-deconvolution {n}x{n} {args.dtype}, 15x15 Gaussian PSF (separable), '
+                        f'K = Gradient(shape) (default kind=centered, edge=True), 0.05*L21Norm; grad F = N x - Conv^T y: '
+                        f'N x by k_sep2d_nrm into a buffer + general-stencil march step (k_pds2d_smarch), '
+                        f'two launches per iteration back to back from C',
+            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+            'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'fkind': r['fkind'],
+            'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
+            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'roofline': {'bound': 'hbm', 'kernel': 'k_pds2d_smarch<centered, NB, L21> (update)',
+                         'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
+                         'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            'nx_roofline': {'bound': 'lds/fp32-vector', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm)',
+                            'kernel_ms': round(km.get('conv_nx', float('nan')), 5), 'flop_per_launch': 116 * N,
+                            'tflops': round(116 * N / (km.get('conv_nx', float('nan')) * 1e-3) / 1e12, 2)}}
 
 
 def slab_bench(n, dtype, K, W, world):
@@ -439,7 +481,9 @@ def slab_bench(n, dtype, K, W, world):
         eng = SlabPDS2D.from_pds(pds, comm, native=True, **kw)
         eng.overlapped()
     except Exception as e:  # noqa: BLE001 -- the torch.distributed-issued loop runs the same kernels
-        print(f'bench: native slab loop unavailable ({e}); torch.distributed per-iteration loop', file=sys.stderr)
+        # reported in the line (top-level 'loop' / 'loop_fallback'), never silent
+        print(f'bench: WARNING native slab loop unavailable ({type(e).__name__}: {e}); falling back to the '
+              f'torch.distributed per-iteration loop (reported as loop_fallback=true)', file=sys.stderr)
         eng = SlabPDS2D.from_pds(pds, comm, native=False, **kw)
     del pds
     torch.cuda.empty_cache()
@@ -487,9 +531,10 @@ def main():
     ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
                     help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
-    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen',
+    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen',
                     help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
-                         'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K); "" skips them')
+                         'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K), c3_cen (C3 with the default '
+                         'centered Gradient); "" skips them')
     ap.add_argument('--lipschitz', default='lanczos', choices=['lanczos', 'analytic'],
                     help='operator norms of the single-GPU 2-D problems: compute_lipschitz_cst() or closed forms')
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
@@ -520,7 +565,9 @@ def main():
         res = slab_bench(n, dtype, K, W, world)
         res['kernel_ms_isolated'] = res['kernel_ms']
     else:
+        t0 = time.perf_counter()
         pds = build_problem(n, n, dtype, lipschitz=args.lipschitz)
+        setup = time.perf_counter() - t0  # phantom, blur, compute_lipschitz_cst of K and Conv (device Lanczos)
         lips = {'K': pds.K.lipschitz_cst, 'Conv': pds.F.map2.lipschitz_cst}
         spec = pds._fused_spec()
         assert spec is not None and spec['fkind'] == 2, 'C3 problem must take the fused separable engine'
@@ -530,6 +577,7 @@ def main():
         # (rocprofv3 kernel-trace average in profiles/ agrees); ms_per_step is the whole loop
         res['kernel_ms'] = res['kernel_ms_isolated'] = res['kernels_ms']['step']
         res['lipschitz'] = lips
+        res['setup_s'] = round(setup, 2)
 
     if rank == 0:
         elem = 4 if dtype == torch.float32 else 8
@@ -559,7 +607,7 @@ def main():
                        'global_shape': [n * world, n], 'parallelism': f'slab{world}' if world > 1 else 'single',
                        'schedule_trial_ms_serial_overlap': res.get('schedule_trial_ms'),
                        'lipschitz': args.lipschitz if world == 1 else 'analytic',
-                       'lipschitz_csts': res.get('lipschitz')},
+                       'lipschitz_csts': res.get('lipschitz'), 'setup_s': res.get('setup_s')},
             'steps_requested': args.steps, 'warmup_requested': args.warmup,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': tsrc,
@@ -577,13 +625,17 @@ def main():
                          'fp32_vector_peak_tflops': 157.3},
             'iteration_GBps': round(alg_bytes / (ms * 1e-3) / 1e9, 1),
         }
+        if 'loop' in res:  # multi-GPU: which slab loop ran (native RCCL loop, or the torch.distributed fallback)
+            out['loop'] = res['loop']
+            out['loop_fallback'] = res['loop'] == 'python'
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:
             out['cpu_baseline'] = None
         if world == 1 and args.engine != 'slab':
             for leg in filter(None, args.legs.split(',')):
-                fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen}[leg]
+                fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen,
+                      'c3_cen': leg_c3_cen}[leg]
                 try:
                     out[leg] = fn(args, dtype, K, W)
                 except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own

@@ -38,6 +38,8 @@ enum { PCS_H_L1 = 0, PCS_H_L21 = 1 };
 enum { PCS_G_NULL = 0, PCS_G_NONNEG = 1, PCS_G_SEGMENT = 2 };
 /* F kinds in the fused step */
 enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3 };
+/* finite-difference K of the fused 2-D steps */
+enum { PCS_K_GRAD_FORWARD = 0, PCS_K_GRAD_BACKWARD = 1, PCS_K_GRAD_CENTERED = 2, PCS_K_LAPLACIAN = 3 };
 
 int pcs_abi_version(void);
 
@@ -246,7 +248,17 @@ typedef struct {
    * = Conv^T (Conv x - y) as four (2 tier + 1)-tap passes. */
   const void* cty;
   const void* ntaps;
+  /* K (appended in ABI 1.1; all zero = the forward Gradient of the fields above).  kkind
+   * PCS_K_GRAD_{FORWARD,BACKWARD,CENTERED}: K = Gradient(kind, edge, step0/1), z = [D0 x; D1 x];
+   * PCS_K_LAPLACIAN: K = w0 D2_0 + w1 D2_1 (Laplacian(weights, step, edge), z has rows*n1
+   * elements, H = lam*L1).  Non-forward K: the general-stencil row-marching kernel (fp32, F = NULL /
+   * DENOISE / GRADBUF, n1 % 4 == 0, 16-B aligned, at least two 64-column strips; slabs need halo
+   * rows x >= 2, y >= 2, z >= 4); PCS_EUNSUPPORTED otherwise (pcs_pds2d_stencil_step covers the rest). */
+  int kkind, edge;
+  double w0, w1;
 } pcs_pds2d_args;
+/* 1 if pcs_pds2d_step runs these arguments (0: PCS_EUNSUPPORTED / invalid). */
+int pcs_pds2d_supported(const pcs_pds2d_args* a);
 int pcs_pds2d_ntaps_len(int half); /* 64 + 32 * tier(half); -1 beyond tier 7 */
 
 int pcs_pds2d_halo_x(int half);
@@ -287,7 +299,6 @@ int64_t pcs_grid_bar_bytes(void);
  * stencils are the standalone operators' (pcs_grad_fwd/adj, pcs_lap_fwd/adj) per element.  With
  * hist/ctrl/ws the last workgroups reduce the partials and run the stopping rule (as
  * pcs_pds2d_step); else only `partials` ([nblocks][4]) is written. */
-enum { PCS_K_GRAD_FORWARD = 0, PCS_K_GRAD_BACKWARD = 1, PCS_K_GRAD_CENTERED = 2, PCS_K_LAPLACIAN = 3 };
 typedef struct {
   int dtype, kkind, fkind, hkind, gkind, edge;
   int64_t n0, n1;

@@ -39,7 +39,8 @@ class PdsArgs(ctypes.Structure):
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('y', _vp), ('gbuf', _vp),
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp),
                 ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64),
-                ('cty', _vp), ('ntaps', _vp)]
+                ('cty', _vp), ('ntaps', _vp),
+                ('kkind', _c_int), ('edge', _c_int), ('w0', _c_dbl), ('w1', _c_dbl)]
 
 
 class StencilArgs(ctypes.Structure):
@@ -123,6 +124,7 @@ _SIGS = {
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
+    'pcs_pds2d_supported': (_c_int, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
     'pcs_pds2d_stencil_nblocks': (_c_i64, [ctypes.POINTER(StencilArgs)]),
     'pcs_pds2d_stencil_ws_bytes': (_c_i64, [ctypes.POINTER(StencilArgs)]),

@@ -26,11 +26,17 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     plain Lanczos in fp64 with O(1) memory: three vectors of ``n`` (q_prev, q, w) plus what
     ``apply`` allocates, no re-orthogonalisation (the extreme Ritz value converges regardless;
     lost orthogonality only duplicates it).  The recurrence coefficients stay on the device
-    (no host sync per step); every ``check_every`` steps the tridiagonal matrix is copied to
-    the host and its extreme eigenvalue computed; the run stops when it moved by at most
-    ``tol`` (relative) since the previous check, or on an invariant subspace (beta ~ 0).
-    Ritz values never exceed the true extreme eigenvalue (up to rounding)."""
-    from scipy.linalg import eigvalsh_tridiagonal
+    (no host sync per step); every ``check_every`` steps the tridiagonal matrix T is copied to
+    the host and its extreme eigenpair (theta, s) computed, with the residual of the Ritz pair
+    r = beta_k |s_k| = ||A y - theta y|| (y the Ritz vector; no extra operator application).
+    The run stops when r <= tol |theta|, when theta moved by at most ``tol`` (relative) since
+    the previous check, or on an invariant subspace (beta ~ 0).
+
+    Returns theta + r: a Ritz value never exceeds the extreme eigenvalue, and some eigenvalue lies
+    within r of it, so the sum is an upper estimate of the extreme eigenvalue (the one the Ritz
+    value approximates) -- PDS step sizes built from it stay inside tau sigma ||K||^2 <= 1
+    (pycsou/opt/proxalgs.py:280-301) instead of exceeding it by the Ritz value's deficit."""
+    from scipy.linalg import eigh_tridiagonal
     dev = O.device()
     g = torch.Generator(device='cpu').manual_seed(seed)
     q = torch.randn(n, generator=g, dtype=torch.float64).to(dev)
@@ -40,7 +46,7 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     alphas = torch.zeros(steps, dtype=torch.float64, device=dev)
     betas = torch.zeros(steps, dtype=torch.float64, device=dev)
     b_prev = torch.zeros((), dtype=torch.float64, device=dev)
-    theta, prev = 0.0, None
+    theta, resid, prev = 0.0, 0.0, None
     for j in range(steps):
         w = apply(q).to(torch.float64)
         a = torch.dot(w, q)
@@ -56,12 +62,19 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
         scale = max(np.max(np.abs(al[np.isfinite(al)]), initial=0.0), 1e-300)
         bad = np.nonzero(~np.isfinite(be) | (be <= 1e-13 * scale))[0]
         k = int(bad[0]) + 1 if bad.size else j + 1  # T of size k: alphas[:k], betas[:k-1]
-        ev = eigvalsh_tridiagonal(al[:k], be[:k - 1]) if k > 1 else al[:1]
-        theta = float(np.max(np.abs(ev))) if sym else float(ev[-1])
-        if bad.size or (prev is not None and abs(theta - prev) <= tol * abs(theta)):
+        if k > 1:
+            ev, S = eigh_tridiagonal(al[:k], be[:k - 1])
+            i = int(np.argmax(np.abs(ev))) if sym else k - 1
+            theta = float(abs(ev[i])) if sym else float(ev[i])
+            # residual of the Ritz pair: the next beta times the last component of its vector
+            resid = 0.0 if bad.size else float(abs(be[k - 1] * S[-1, i]))
+        else:
+            theta, resid = (float(abs(al[0])) if sym else float(al[0])), (0.0 if bad.size else float(abs(be[0])))
+        if (bad.size or resid <= tol * abs(theta)
+                or (prev is not None and abs(theta - prev) <= tol * abs(theta))):
             break
         prev = theta
-    return theta
+    return theta + resid
 
 
 class LinearOperator(DifferentiableMap):
@@ -153,8 +166,9 @@ class LinearOperator(DifferentiableMap):
         """Operator norm ``||K||_2`` (``pycsou/core/linop.py:279-321``: ARPACK ``svds`` / ``eigsh``
         with k=1) by device Lanczos on ``K^T K`` (or ``|eig|`` if symmetric) in bounded memory
         (a few vectors of the domain size, whatever the operator's size).  Other ARPACK keyword
-        arguments are accepted and ignored; ``tol`` is the relative change of the estimate
-        between checks at which the iteration stops."""
+        arguments are accepted and ignored; ``tol`` is the relative residual (or change of the
+        estimate between checks) at which the iteration stops.  The value is an upper estimate
+        (Ritz value + residual bound, see _lanczos_extreme), so step sizes from it are safe."""
         if self.is_symmetric:
             lam = _lanczos_extreme(lambda v: self._apply(v), self.shape[1], sym=True, tol=tol, max_steps=max_steps)
             self.lipschitz_cst = float(abs(lam))

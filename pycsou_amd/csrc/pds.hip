@@ -11,6 +11,7 @@
 #include "pds_march.hpp"
 #include "pds_nmarch.hpp"
 #include "pds_pt.hpp"
+#include "pds_smarch.hpp"
 
 namespace pcs {
 
@@ -393,8 +394,129 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, rb, st) : launch_pt<FK, PCS_H_L1>(a, rb, st);
 }
 
-// the row-marching families (march, pt) take row bands; the tile kernel runs whole slabs only
+// ---- fp32 general-stencil K (backward / centred Gradient, Laplacian) with a pointwise grad F:
+// the row-marching kernel of pds_smarch.hpp (PCS_SM_FWD=1 also routes the forward Gradient
+// through it: diagnostics / A-B against pds_pt.hpp)
+static bool sm_forward() {
+  const char* e = getenv("PCS_SM_FWD");  // read per call (tests switch it)
+  return e != nullptr && atoi(e) != 0;
+}
+
+static int sm_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_smarch<PCS_CENTERED, PCS_F_DENOISE, PCS_H_L21>, 256,
+                                                     0) != hipSuccess ||
+        nb < 1)
+      nb = 3;
+    (void)hipGetLastError();
+    slots = cus * (nb < 3 ? nb : 3);  // as the pt kernel: fewer, longer row segments
+    const char* e = getenv("PCS_SM_SLOTS");  // diagnostics: grid-size sweep
+    if (e && atoi(e) > 0) slots = atoi(e);
+  }
+  return slots;
+}
+
+static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
+  const int tiles_x = (int)((a->n1 + 63) / 64);
+  if (tiles_x < 2) return false;
+  plan_bands(rb, 16, tiles_x, sm_slots(), 4, p);
+  return true;
+}
+
+// F = (1/2)||Conv x - y||^2, Conv separable, with a non-forward K: grad F = N x - Conv^T y, N x by the
+// in-plane normal-operator kernel into gbuf (pcs_conv2d_sep_ata_planes on the whole image: two
+// composite-tap passes), then the march step reads gbuf and cty -- whole images only
+static bool sm_normal(const pcs_pds2d_args* a) {
+  if (a->fkind != PCS_F_SEPCONV || !a->cty || !a->gbuf || !aligned16(a->cty) || a->rows != a->n0) return false;
+  if (a->half < 0 || a->half > 7 || !a->taps0 || !a->taps1) return false;
+  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 0, a->n0, a->n1, a->taps0, 2 * a->half + 1, a->half,
+                                   a->taps1, 2 * a->half + 1, a->half, nullptr) == PCS_OK;
+}
+
+static bool use_smarch(const pcs_pds2d_args* a) {
+  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward()) return false;
+  if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return false;
+  if (a->dtype != PCS_F32 || !make_slab(a).vec) return false;
+  if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF &&
+      !(a->kkind != PCS_K_GRAD_FORWARD && sm_normal(a)))
+    return false;
+  if (a->hkind != PCS_H_L1 && (a->hkind != PCS_H_L21 || a->kkind == PCS_K_LAPLACIAN)) return false;
+  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
+                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
+  MarchPlan p;
+  return sm_plan(a, full_bands(a), &p);
+}
+
+static SParams make_sparams(const pcs_pds2d_args* a) {
+  SParams Q;
+  Q.ih20 = (float)(1.0 / (a->step0 * a->step0));
+  Q.ih21 = (float)(1.0 / (a->step1 * a->step1));
+  Q.w0 = (float)a->w0;
+  Q.w1 = (float)a->w1;
+  Q.edge = a->edge != 0;
+  return Q;
+}
+
+template <int KK, int FK, int HK>
+static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  MarchPlan p;
+  if (!sm_plan(a, rb, &p)) return PCS_EINVAL;
+  if (p.ntasks == 0) return PCS_OK;
+  const Slab s64 = make_slab(a);
+  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
+  const Params<float> P = make_params<float>(a);
+  const float* g = FK == PCS_F_DENOISE                       ? (const float*)a->y
+                   : (FK == PCS_F_GRADBUF || FK == SM_F_NB) ? (const float*)a->gbuf
+                                                            : nullptr;
+  const float* b = FK == SM_F_NB ? (const float*)a->cty : nullptr;
+  k_pds2d_smarch<KK, FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
+      (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, g, b, s, P, make_sparams(a), a->gkind,
+      a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
+  return launch_status();
+}
+
+template <int KK, int FK>
+static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  if constexpr (KK == SK_LAP) return launch_smarch<KK, FK, PCS_H_L1>(a, rb, st);
+  else
+    return a->hkind == PCS_H_L21 ? launch_smarch<KK, FK, PCS_H_L21>(a, rb, st)
+                                 : launch_smarch<KK, FK, PCS_H_L1>(a, rb, st);
+}
+
+template <int KK>
+static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  if (a->fkind == PCS_F_SEPCONV) {  // N x -> gbuf, then the step with grad F = gbuf - cty
+    if (KK == PCS_FORWARD || rb.ra0 != 0 || rb.rb1 != a->rows) return PCS_EUNSUPPORTED;
+    const int rc = pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 1, a->n0, a->n1, a->taps0, 2 * a->half + 1,
+                                             a->half, a->taps1, 2 * a->half + 1, a->half, st);
+    if (rc != PCS_OK) return rc;
+    return launch_smarch<KK, SM_F_NB>(a, rb, st);
+  }
+  if (a->fkind == PCS_F_DENOISE) return launch_smarch<KK, PCS_F_DENOISE>(a, rb, st);
+  if (a->fkind == PCS_F_GRADBUF) return launch_smarch<KK, PCS_F_GRADBUF>(a, rb, st);
+  return launch_smarch<KK, PCS_F_NULL>(a, rb, st);
+}
+
+static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  switch (a->kkind) {
+    case PCS_K_GRAD_FORWARD: return launch_smarch<PCS_FORWARD>(a, rb, st);
+    case PCS_K_GRAD_BACKWARD: return launch_smarch<PCS_BACKWARD>(a, rb, st);
+    case PCS_K_GRAD_CENTERED: return launch_smarch<PCS_CENTERED>(a, rb, st);
+    case PCS_K_LAPLACIAN: return launch_smarch<SK_LAP>(a, rb, st);
+    default: return PCS_EINVAL;
+  }
+}
+
+// the row-marching families (march, pt, smarch) take row bands; the tile kernel runs whole slabs only
 static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  if (use_smarch(a)) return launch_smarch(a, rb, st);
+  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, rb, st) : launch_march<7>(a, rb, st);
   if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, rb, st);
   if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, rb, st);
@@ -403,6 +525,8 @@ static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
+  if (use_smarch(a)) return pds2d_bands(a, full_bands(a), st);
+  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (use_march(a) || use_pt(a)) return pds2d_bands(a, full_bands(a), st);
   switch (a->fkind) {
     case PCS_F_NULL: return launch_pds2d<T, PCS_F_NULL, 0>(a, st);
@@ -422,6 +546,11 @@ static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
 
 static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb) {
   MarchPlan p;
+  if (use_smarch(a)) {
+    sm_plan(a, rb, &p);
+    return (int64_t)p.ntasks;
+  }
+  if (a->kkind != PCS_K_GRAD_FORWARD) return -1;
   if (use_march(a)) {
     if (tier_for(a->half) == 3) march_plan<3>(a, rb, &p);
     else march_plan<7>(a, rb, &p);
@@ -455,6 +584,7 @@ int pcs_pds2d_ntaps_len(int half) {
 
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
   if (!a || a->rows < 1 || a->n1 < 1) return -1;
+  if (use_smarch(a) || a->kkind != PCS_K_GRAD_FORWARD) return bands_nblocks(a, full_bands(a));
   if (use_march(a) || use_pt(a)) return bands_nblocks(a, full_bands(a));
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);
@@ -476,6 +606,11 @@ static int check_args(const pcs_pds2d_args* a) {
   if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return PCS_EINVAL;
   if (a->gkind < PCS_G_NULL || a->gkind > PCS_G_SEGMENT) return PCS_EINVAL;
   if (!(a->sigma > 0) || !(a->step0 != 0) || !(a->step1 != 0)) return PCS_EINVAL;
+  if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return PCS_EINVAL;
+  if (a->kkind == PCS_K_LAPLACIAN && a->hkind != PCS_H_L1) return PCS_EINVAL;  // one component: L21 == L1
+  if (a->kkind != PCS_K_GRAD_FORWARD && a->rows < a->n0 &&
+      (a->halo_x < 2 || a->halo_z < 4 || (a->fkind != PCS_F_NULL && a->halo_y < 2)))
+    return PCS_EINVAL;
   if ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_SEPCONV) && !a->y) return PCS_EINVAL;
   if (a->fkind == PCS_F_GRADBUF && !a->gbuf) return PCS_EINVAL;
   if (a->fkind == PCS_F_SEPCONV && (!a->taps0 || !a->taps1 || a->half < 0)) return PCS_EINVAL;
@@ -503,8 +638,15 @@ int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int6
   const int rc = check_args(a);
   if (rc != PCS_OK) return rc;
   if (a->hist || !bands_ok(a, ra0, rb0, ra1, rb1)) return PCS_EINVAL;
-  if (!(use_march(a) || use_pt(a))) return PCS_EUNSUPPORTED;
+  if (!(use_smarch(a) || (a->kkind == PCS_K_GRAD_FORWARD && (use_march(a) || use_pt(a))))) return PCS_EUNSUPPORTED;
   return pds2d_bands(a, RowBands{ra0, rb0, ra1, rb1}, st);
+}
+
+int pcs_pds2d_supported(const pcs_pds2d_args* a) {
+  if (check_args(a) != PCS_OK) return 0;
+  if (a->kkind != PCS_K_GRAD_FORWARD) return use_smarch(a) ? 1 : 0;
+  if (use_smarch(a) || use_march(a) || use_pt(a)) return 1;
+  return (a->dtype == PCS_F32 || a->dtype == PCS_F64) && (a->fkind != PCS_F_SEPCONV || tier_for(a->half) > 0) ? 1 : 0;
 }
 
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
@@ -542,7 +684,8 @@ int pcs_pds2d_run_persistent(const pcs_pds2d_args* a, int64_t n, void* bar, hipS
   if (!a || n < 0 || n > 0x7fffffff || !a->hist || !bar || !aligned16(bar)) return PCS_EINVAL;
   const int rc = check_args(a);
   if (rc != PCS_OK) return rc;
-  if (a->rows != a->n0 || use_march(a) || !use_pt(a)) return PCS_EUNSUPPORTED;
+  if (a->rows != a->n0 || a->kkind != PCS_K_GRAD_FORWARD || use_smarch(a) || use_march(a) || !use_pt(a))
+    return PCS_EUNSUPPORTED;
   if (n == 0) return PCS_OK;
   unsigned* b = (unsigned*)bar;
   if (a->fkind == PCS_F_DENOISE) return launch_pt_loop<PCS_F_DENOISE>(a, n, b, st);

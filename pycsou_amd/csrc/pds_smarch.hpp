@@ -1,0 +1,443 @@
+// Row-marching fused 2-D PDS step for a GENERAL finite-difference K (fp32, pointwise grad F):
+//   K = Gradient(kind = 'backward' | 'centered' | 'forward', edge, sampling)   (pycsou/linop/diff.py:777-882;
+//       'centered' is the reference's default), z = [D0 x; D1 x]
+//   K = Laplacian(weights, sampling, edge) = w0 D2_0 + w1 D2_1                (diff.py:885-957), z = K x
+// F = NULL (0), DENOISE (grad F = x - y), GRADBUF (grad F read from g) or, for a separable blur,
+// grad F = N x - Conv^T y with N x from a buffer (SM_F_NB, below), H = lam L1 / lam L21.
+// PrimalDualSplitting.update_iterand / update_diagnostics (pycsou/opt/proxalgs.py:343-394):
+//   x_t = prox_G((x - tau grad F) - tau K^T z),  u = 2 x_t - x,  x' = rho x_t + (1 - rho) x
+//   z'  = rho H.fenchel_prox(z + sigma K u, sigma) + (1 - rho) z
+//
+// The forward-Gradient row march (pds_pt.hpp) generalised to stencils that reach one sample
+// both ways (two at the image edges for the Laplacian's one-sided rows).  One workgroup
+// (256 threads: 4 rows x 16 four-column groups per wave) owns a 64-column strip of a row segment
+// [s0, s1) and marches down it 16 rows per step (a = s0 + 16 k):
+//   top   land z rows [a + ZHI - 15, a + ZHI] (loaded during the previous step) in the z ring;
+//         issue the next step's z loads
+//   U     rows [a+1, a+16]: K^T z from the z ring, x_t, u -> u ring, x' -> HBM.  Every item also
+//         computes a fifth column: c0 - 1 (group 0) or c + 4 (the rest; group 15's is c0 + 64),
+//         the u columns K u of the strip's edge columns reaches; issue the next step's x, y|g
+//   Z     rows [a, a+16): K u from the u ring, fenchel prox, relaxation, z' -> HBM
+// z and u live in 32-row LDS rings (row r in slot r & 31; columns [c0 - 4, c0 + 68)), so every
+// z row is read from HBM once per strip, every u row computed once; x and y|g are read once.
+// HBM traffic per pixel: x, y|g, z (D components) in; x', z' out -- (3 + 2 D) words when F reads
+// a buffer (7 for the gradients, 5 for the Laplacian), plus the strips' 4-column halos of z.
+// A one-row-deep prologue (rows s0 - 2 .. s0 of u, masked loads) starts each segment.
+// Per element the stencils are stencil.hpp's (same operation order), 1/h applied as a
+// multiplication (exact for unit sampling).  Global accesses go through buffer descriptors
+// (hardware range check: rows / columns outside the image or the stored slab read 0).
+#pragma once
+
+#include <type_traits>
+
+#include "pds_march.hpp"
+
+namespace pcs {
+
+enum { SK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED (2 components) or the Laplacian (1)
+// FK beyond the public kinds: grad F = g - b with g = N x = Conv^T Conv x from a buffer (the in-plane
+// normal-operator kernel, pcs_conv2d_sep_ata_planes) and b = Conv^T y (formed once per problem)
+enum { SM_F_NB = 16 };
+
+// ---- the stencils on a 5-sample window w[k] = a[i + k - 2] along one axis (stencil.hpp order);
+// INT: the sample is known to lie >= 2 samples inside the axis (no edge rule applies)
+template <int KIND, bool INT>
+__device__ __forceinline__ float sw_d1_fwd(const float (&w)[5], int i, int n, float ih, int edge) {
+  if constexpr (KIND == PCS_FORWARD) {
+    const float c = (w[3] - w[2]) * ih;
+    return (INT || i < n - 1) ? c : 0.f;
+  } else if constexpr (KIND == PCS_BACKWARD) {
+    const float c = (w[2] - w[1]) * ih;
+    return (INT || i > 0) ? c : 0.f;
+  } else {
+    const float c = (0.5f * w[3] - 0.5f * w[1]) * ih;
+    if constexpr (INT) return c;
+    const float e = (i == 0) ? (w[3] - w[2]) * ih : (w[2] - w[1]) * ih;
+    return (i > 0 && i < n - 1) ? c : ((edge && n >= 2) ? e : 0.f);
+  }
+}
+template <int KIND, bool INT>
+__device__ __forceinline__ float sw_d1_adj(const float (&w)[5], int i, int n, float ih, int edge) {
+  float acc = 0.f;
+  if constexpr (KIND == PCS_FORWARD) {
+    if (INT || i < n - 1) acc -= w[2] * ih;
+    if (INT || i > 0) acc += w[1] * ih;
+  } else if constexpr (KIND == PCS_BACKWARD) {
+    if (INT || i < n - 1) acc -= w[3] * ih;
+    if (INT || i > 0) acc += w[2] * ih;
+  } else {
+    if (INT || i <= n - 3) acc -= (0.5f * w[3]) * ih;
+    if (INT || i >= 2) acc += (0.5f * w[1]) * ih;
+    if (!INT && edge && n >= 2) {
+      if (i == 0) acc -= w[2] * ih;
+      if (i == 1) acc += w[1] * ih;
+      if (i == n - 2) acc -= w[3] * ih;
+      if (i == n - 1) acc += w[2] * ih;
+    }
+  }
+  return acc;
+}
+template <bool INT>
+__device__ __forceinline__ float sw_d2_fwd(const float (&w)[5], int i, int n, float ih2, int edge) {
+  const float c = (w[3] - 2.f * w[2] + w[1]) * ih2;
+  if constexpr (INT) return c;
+  const float e = (i == 0) ? (w[2] - 2.f * w[3] + w[4]) * ih2 : (w[0] - 2.f * w[1] + w[2]) * ih2;
+  return (i > 0 && i < n - 1) ? c : ((edge && n >= 3) ? e : 0.f);
+}
+template <bool INT>
+__device__ __forceinline__ float sw_d2_adj(const float (&w)[5], int i, int n, float ih2, int edge) {
+  float acc = 0.f;
+  if (INT || i <= n - 3) acc += w[3] * ih2;
+  if (INT || (i >= 1 && i <= n - 2)) acc -= (2.f * w[2]) * ih2;
+  if (INT || i >= 2) acc += w[1] * ih2;
+  if (!INT && edge && n >= 3) {
+    if (i == 0) acc += w[2] * ih2;
+    if (i == 1) acc -= (2.f * w[1]) * ih2;
+    if (i == 2) acc += w[0] * ih2;
+    if (i == n - 3) acc += w[4] * ih2;
+    if (i == n - 2) acc -= (2.f * w[3]) * ih2;
+    if (i == n - 1) acc += w[2] * ih2;
+  }
+  return acc;
+}
+
+// stencil-specific parameters (the rest is Params<float>)
+struct SParams {
+  float ih20, ih21, w0, w1;  // 1 / sampling^2 per axis, Laplacian weights
+  int edge;
+};
+
+template <int KK>
+struct SMarch {
+  static constexpr int TW = 64, TS = 16, D = KK == SK_LAP ? 1 : 2;
+  // z rows [a + ZLO, a + ZHI] feed step a (U rows a+1..a+16 reach ZR rows up, ZD down; the Z
+  // rows a..a+15 read their own z)
+  static constexpr int ZHI = KK == SK_LAP ? 18 : KK == PCS_FORWARD ? 16 : 17;
+  // rows of u above a segment the first Z rows read (the prologue computes them) and the z rows
+  // above those that u needs
+  static constexpr int UPRO = KK == SK_LAP ? 2 : 1, ZPRO = UPRO + (KK == SK_LAP ? 2 : 1);
+  // u / z windows along axis 0 (offsets -2..+2 from the row): which rows each phase reads
+  static constexpr bool UWIN(int k) {  // U phase: z rows r - 2 + k
+    return KK == SK_LAP ? true : KK == PCS_FORWARD ? (k == 1 || k == 2) : KK == PCS_BACKWARD ? (k == 2 || k == 3)
+                                                                                             : (k >= 1 && k <= 3);
+  }
+  static constexpr bool ZWIN(int k) {  // Z phase: u rows r - 2 + k
+    return KK == SK_LAP ? true : KK == PCS_FORWARD ? (k == 2 || k == 3) : KK == PCS_BACKWARD ? (k == 1 || k == 2)
+                                                                                             : (k >= 1 && k <= 3);
+  }
+  // K u reaches left / right along axis 1 (the neighbour groups the Z phase reads; the U phase
+  // reads both, its fifth column lying on either side)
+  static constexpr bool Z_L = KK != PCS_FORWARD, Z_R = KK != PCS_BACKWARD;  // u[c-1] / u[c+1]
+  static constexpr int RING = 32, WZ = TW + 12, GZ = 18;  // ring rows of columns [c0 - 4, c0 + 68) (+ pad: 19 slots)
+  static constexpr int NZN = TS * GZ;                     // z items per component per step
+  static constexpr int O_Z = 0, O_U = D * RING * WZ, SZ = O_U + RING * WZ;
+};
+
+template <int KK, int FK, int HK, bool CI>
+__device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* __restrict__ xn,
+                                            const float* __restrict__ z, float* __restrict__ zn,
+                                            const float* __restrict__ gsrc, const float* __restrict__ bsrc,
+                                            const Slab32& s, const Params<float>& P,
+                                            const SParams& Q, int gk, int s0, int s1, int c0, float* sm,
+                                            double (&part)[4]) {
+  using T = float;
+  using M = SMarch<KK>;
+  constexpr int NT = 256, TS = M::TS, TW = M::TW, WZ = M::WZ, GZ = M::GZ, D = M::D, RING = M::RING;
+  constexpr int KZ = cdiv(M::NZN, NT);
+  T* ZR = sm + M::O_Z;  // component d, row r: ZR + d * RING * WZ + (r & 31) * WZ; column c at c - c0 + 4
+  T* UR = sm + M::O_U;
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hb = tid >> 5, l5 = tid & 31;
+  const int ui = 2 * hb + lane_grp(l5), ug = lane_idx(l5);  // both phases: row ui of the step, group ug
+  const int n0 = s.n0, n1 = s.n1, edge = Q.edge;
+  const int zstride = (s.rows + 2 * s.hz) * n1;
+  const View vx = make_view(x, s, s.hx), vg = make_view(gsrc != nullptr ? gsrc : x, s, s.hy),
+             vb = make_view(bsrc != nullptr ? bsrc : x, s, s.hy);
+  View vz[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) vz[d] = make_view(z + d * zstride, s, s.hz);
+  const uint32_t pitch = (uint32_t)n1 * 4u;
+  const Rsrc rxn = rsrc_of(xn, (uint32_t)(s.rows + 2 * s.hx) * pitch);
+  Rsrc rzn[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rzn[d] = rsrc_of(zn + d * zstride, (uint32_t)zstride * 4u);
+#define PCS_WAVE_ON(k, N) ((k) * NT + wv * 64 < (N))
+#define PCS_ITEM(k, N) min((k) * NT + tid, (N) - 1)
+
+  // rings start zeroed: the columns no item writes (c0 - 4 .. c0 - 2, c0 + 65 ..) read as 0
+  {
+    const G4<T> zero = {{T(0), T(0), T(0), T(0)}};
+    for (int i = tid; i < M::SZ / 4; i += NT) st4(sm + 4 * i, zero);
+  }
+  const int c = c0 + 4 * ug;
+  const int ce = ug == 0 ? c - 1 : c + 4;             // the item's fifth column
+  const int lc = 4 + 4 * ug, lce = ug == 0 ? 3 : lc + 4;  // their ring columns
+  const bool ext_st = ug == 0 || ug == TW / 4 - 1;   // fifth columns K u reads: c0 - 1, c0 + 64
+  const uint32_t co_c = col_off(c, n1), co_e = col_off(ce, n1);
+  // CI: the strip and its 4-column margins lie >= 2 columns inside the image (no column edge rule)
+  const bool cin = CI || c < n1, ce_in = CI || (unsigned)ce < (unsigned)n1;
+  uint32_t co_z[KZ];
+  int rr_z[KZ], lo_z[KZ];
+#pragma unroll
+  for (int k = 0; k < KZ; ++k) {
+    const int e = PCS_ITEM(k, M::NZN), g = e - (e / GZ) * GZ;
+    rr_z[k] = e / GZ;
+    lo_z[k] = 4 * g;
+    co_z[k] = col_off(c0 - 4 + 4 * g, n1);
+  }
+  G4<T> zr[D][KZ], xr, gr, br;
+  T xe = T(0), ge = T(0), be = T(0);
+  // z rows [a + ZHI - 15, a + ZHI] (rows below rmin read as 0)
+  auto loads_z = [&](int a, int rmin) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int k = 0; k < KZ; ++k) {
+        const int r = a + M::ZHI - 15 + rr_z[k];
+        zr[d][k] = bload4(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
+      }
+  };
+  auto land_z = [&](int a) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int k = 0; k < KZ; ++k)
+        if (PCS_WAVE_ON(k, M::NZN))
+          st4(ZR + d * RING * WZ + ((a + M::ZHI - 15 + rr_z[k]) & 31) * WZ + lo_z[k], zr[d][k]);
+  };
+  // x and y|g of U row a + 1 + ui: the group and the fifth column
+  auto loads_x = [&](int a, int rmin) {
+    const int r = a + 1 + ui;
+    const uint32_t ro = r < rmin ? kOOB : vx.row_off(r);
+    xr = bload4(vx.r, ro + co_c);
+    xe = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vx.r, (int)(ro + co_e), 0, 0));
+    if constexpr (FK != PCS_F_NULL) {
+      const uint32_t rg = r < rmin ? kOOB : vg.row_off(r);
+      gr = bload4(vg.r, rg + co_c);
+      ge = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vg.r, (int)(rg + co_e), 0, 0));
+    }
+    if constexpr (FK == SM_F_NB) {
+      const uint32_t rb = r < rmin ? kOOB : vb.row_off(r);
+      br = bload4(vb.r, rb + co_c);
+      be = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(rb + co_e), 0, 0));
+    }
+  };
+
+  // ---- U: x_t, u on row lr = a + 1 + ui, columns c .. c + 3 and ce; x' on own cells
+  // RI (std::true_type / false_type): every row of the step lies >= 2 rows inside the image
+  auto uphase = [&](auto ri, int a) {
+    constexpr bool RI = decltype(ri)::value;
+    const int lr = a + 1 + ui, gr_ = s.row0 + lr;
+    const T* Z0 = ZR;
+    const T* Z1 = ZR + (D - 1) * RING * WZ;  // the axis-1 component (the Laplacian's only one)
+    G4<T> v0[5];
+    T ve[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const T* row = Z0 + ((lr - 2 + k) & 31) * WZ;
+      if (M::UWIN(k)) {
+        v0[k] = lds4(row + lc);
+        ve[k] = row[lce];
+      } else {
+        v0[k] = G4<T>{{T(0), T(0), T(0), T(0)}};
+        ve[k] = T(0);
+      }
+    }
+    const T* hrow = Z1 + (lr & 31) * WZ;
+    const G4<T> hl = lds4(hrow + lc - 4);
+    const G4<T> hc = D == 2 ? lds4(hrow + lc) : v0[2];
+    const G4<T> hr = lds4(hrow + lc + 4);
+    const T hv[12] = {hl.v[0], hl.v[1], hl.v[2], hl.v[3], hc.v[0], hc.v[1],
+                      hc.v[2], hc.v[3], hr.v[0], hr.v[1], hr.v[2], hr.v[3]};
+    const bool rrow = RI || (unsigned)gr_ < (unsigned)n0;
+    const bool own = lr >= s0 && lr < s1 && rrow && cin;
+    G4<T> uo, xo;
+    T ue = T(0), sdx = T(0), sx = T(0);
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      const int i1 = m < 4 ? c + m : ce;
+      T w0[5], w1[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        w0[k] = m < 4 ? v0[k].v[m] : ve[k];
+        w1[k] = m < 4 ? hv[2 + m + k] : (ug == 0 ? hv[1 + k] : hv[6 + k]);
+      }
+      T kt;
+      if constexpr (KK == SK_LAP) {
+        kt = Q.w0 * sw_d2_adj<RI>(w0, gr_, n0, Q.ih20, edge) + Q.w1 * sw_d2_adj<CI>(w1, i1, n1, Q.ih21, edge);
+      } else {  // VStack rmatvec: (0 + D0^T z0) + D1^T z1
+        kt = T(0) + sw_d1_adj<KK, RI>(w0, gr_, n0, P.inv_step0, edge);
+        kt += sw_d1_adj<KK, CI>(w1, i1, n1, P.inv_step1, edge);
+      }
+      const T xv = m < 4 ? xr.v[m] : xe;
+      T gf = T(0);
+      if constexpr (FK == PCS_F_DENOISE) gf = xv - (m < 4 ? gr.v[m] : ge);  // (2 (x + (-y))) 0.5, exact
+      else if constexpr (FK == PCS_F_GRADBUF) gf = m < 4 ? gr.v[m] : ge;
+      else if constexpr (FK == SM_F_NB) gf = (m < 4 ? gr.v[m] : ge) - (m < 4 ? br.v[m] : be);
+      const T xt = prox_g((xv - P.tau * gf) - P.tau * kt, gk, P.seg_a, P.seg_b);
+      const bool in = rrow && (m < 4 ? cin : ce_in);
+      const T u = in ? (T(2) * xt - xv) : T(0);
+      if (m < 4) {
+        uo.v[m] = u;
+        const T xnew = P.rho * xt + P.omr * xv;
+        xo.v[m] = xnew;
+        const T dx = xv - xnew;
+        sdx += dx * dx;
+        sx += xv * xv;
+      } else {
+        ue = u;
+      }
+    }
+    if (own) {
+      part[0] += (double)sdx;
+      part[1] += (double)sx;
+    }
+    T* urow = UR + (lr & 31) * WZ;
+    st4(urow + lc, uo);
+    if (ext_st) urow[lce] = ue;
+    bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
+  };
+
+  // ---- Z: z' on row lr = a + ui, columns c .. c + 3
+  auto zphase = [&](auto ri, int a) {
+    constexpr bool RI = decltype(ri)::value;
+    const int lr = a + ui, gr_ = s.row0 + lr;
+    G4<T> v0[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      v0[k] = M::ZWIN(k) ? lds4(UR + ((lr - 2 + k) & 31) * WZ + lc) : G4<T>{{T(0), T(0), T(0), T(0)}};
+    const T* hrow = UR + (lr & 31) * WZ;
+    const G4<T> zero = {{T(0), T(0), T(0), T(0)}};
+    const G4<T> hl = M::Z_L ? lds4(hrow + lc - 4) : zero;
+    const G4<T> hc = v0[2];
+    const G4<T> hr = M::Z_R ? lds4(hrow + lc + 4) : zero;
+    const T hv[12] = {hl.v[0], hl.v[1], hl.v[2], hl.v[3], hc.v[0], hc.v[1],
+                      hc.v[2], hc.v[3], hr.v[0], hr.v[1], hr.v[2], hr.v[3]};
+    G4<T> zv[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) zv[d] = lds4(ZR + d * RING * WZ + (lr & 31) * WZ + lc);
+    const bool own = lr >= s0 && lr < s1 && (RI || (unsigned)gr_ < (unsigned)n0) && cin;
+    G4<T> o[D];
+    T sdz = T(0), sz = T(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int i1 = c + m;
+      T w0[5], w1[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        w0[k] = v0[k].v[m];
+        w1[k] = hv[2 + m + k];
+      }
+      T ku[D];
+      if constexpr (KK == SK_LAP) {  // w0 D2_0 u + w1 D2_1 u (pylops Laplacian matvec)
+        ku[0] = Q.w0 * sw_d2_fwd<RI>(w0, gr_, n0, Q.ih20, edge) + Q.w1 * sw_d2_fwd<CI>(w1, i1, n1, Q.ih21, edge);
+      } else {
+        ku[0] = sw_d1_fwd<KK, RI>(w0, gr_, n0, P.inv_step0, edge);
+        ku[D - 1] = sw_d1_fwd<KK, CI>(w1, i1, n1, P.inv_step1, edge);
+      }
+      T w[D], v[D], zt[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        w[d] = zv[d].v[m] + P.sigma * ku[d];
+        v[d] = w[d] * P.inv_sigma;
+      }
+      if constexpr (D == 2 && HK == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
+        T f = T(1) - P.t_h * fast_rsqrt(v[0] * v[0] + v[D - 1] * v[D - 1]);
+        f = f > T(0) ? f : T(0);
+#pragma unroll
+        for (int d = 0; d < D; ++d) zt[d] = w[d] - P.sigma * (f * v[d]);
+      } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
+#pragma unroll
+        for (int d = 0; d < D; ++d) zt[d] = w[d] - P.sigma * (v[d] - P.t_h * clip1(v[d] * P.inv_t_h));
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        o[d].v[m] = P.rho * zt[d] + P.omr * zv[d].v[m];
+        const T ed = zv[d].v[m] - o[d].v[m];
+        sdz += ed * ed;
+        sz += zv[d].v[m] * zv[d].v[m];
+      }
+    }
+    if (own) {
+      part[2] += (double)sdz;
+      part[3] += (double)sz;
+    }
+    const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_c;
+#pragma unroll
+    for (int d = 0; d < D; ++d) bstore4(rzn[d], off, o[d]);
+  };
+
+  // prologue: u on rows [s0 - UPRO, s0] (a pseudo-step at a = s0 - TS whose loads skip the rows
+  // it does not need), x' on row s0
+  const int nsteps = (s1 - s0 + TS - 1) / TS;
+  loads_z(s0 - TS, s0 - M::ZPRO);
+  loads_x(s0 - TS, s0 - M::UPRO);
+  lds_barrier();  // rings zeroed
+  land_z(s0 - TS);
+  if (nsteps > 0) loads_z(s0, -(1 << 30));
+  lds_barrier();
+  uphase(std::false_type{}, s0 - TS);
+  if (nsteps > 0) loads_x(s0, -(1 << 30));
+  for (int k = 0; k < nsteps; ++k) {
+    const int a = s0 + k * TS;
+    // rows [a, a + 16] at >= 2 rows from both image edges (uniform)
+    const bool ri = s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0;
+    lds_barrier();  // the previous step's Z phase is done with the rings
+    land_z(a);
+    __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU (as pds_pt.hpp)
+    if (k + 1 < nsteps) loads_z(a + TS, -(1 << 30));
+    __builtin_amdgcn_s_setprio(0);
+    lds_barrier();
+    if (ri) uphase(std::true_type{}, a);
+    else uphase(std::false_type{}, a);
+    __builtin_amdgcn_s_setprio(3);
+    if (k + 1 < nsteps) loads_x(a + TS, -(1 << 30));
+    __builtin_amdgcn_s_setprio(0);
+    lds_barrier();
+    if (ri) zphase(std::true_type{}, a);
+    else zphase(std::false_type{}, a);
+  }
+#undef PCS_WAVE_ON
+#undef PCS_ITEM
+}
+
+template <int KK, int FK, int HK>
+__global__ __launch_bounds__(256) void k_pds2d_smarch(const float* __restrict__ x, float* __restrict__ xn,
+                                                       const float* __restrict__ z, float* __restrict__ zn,
+                                                       const float* __restrict__ gsrc,
+                                                       const float* __restrict__ bsrc, Slab32 s, Params<float> P,
+                                                       SParams Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
+                                                       double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
+                                                       int ntasks) {
+  __shared__ __attribute__((aligned(16))) float sm[SMarch<KK>::SZ];
+  __shared__ double red[4 * 4];
+  __shared__ int flag[2];
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
+  int task;
+  {  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
+    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int seg = task / tiles_x, strip = task - seg * tiles_x;
+  int s0, s1;
+  band_rows(bd, seg, s0, s1);
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  const int c0 = strip * SMarch<KK>::TW;
+  if (!stopped) {
+    if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
+      smarch_task<KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+    else
+      smarch_task<KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+  }
+  block_sum<4>(part, red);
+  if (hist != nullptr || ro.sums != nullptr) {
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
+  } else if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
+  }
+}
+
+}  // namespace pcs

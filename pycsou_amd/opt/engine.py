@@ -505,36 +505,80 @@ class PDS2DStencilEngine(PDS2DEngine):
         self.Z = [z0.to(dtype).clone(), torch.empty(nc * N, dtype=dtype, device=dev)]
         self.chunk = max(2, chunk + (chunk % 2))
         self.use_graph = use_graph
-        a = L.StencilArgs()
-        a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
-        a.kkind, a.hkind, a.gkind, a.edge = spec['kkind'], spec['hkind'], spec['gkind'], int(spec['edge'])
-        a.n0, a.n1 = n0, n1
-        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
-        a.step0, a.step1 = spec['steps']
-        a.w0, a.w1 = spec['weights']
-        a.seg_a, a.seg_b = spec['seg']
         fk = spec['fkind']
         self.conv = None
         if fk in (L.PCS_F_DENOISE, L.PCS_F_GRADBUF):
             self.y = -O.to_dev(spec['shift'], dtype)  # y = -shift exactly
-            a.g = self.y.data_ptr()
         if fk == L.PCS_F_GRADBUF:
             conv = self.conv = spec['conv']
             conv._h.get(dtype), conv._hf.get(dtype)
             self.plans = (conv.plan(dtype, False), conv.plan(dtype, True))
             self.R = torch.empty(N, dtype=dtype, device=dev)
             self.Gb = torch.empty(N, dtype=dtype, device=dev)
-            a.g = self.Gb.data_ptr()
-        a.fkind = self.fkind = fk
+        gsrc = None if fk == L.PCS_F_NULL else (self.Gb if fk == L.PCS_F_GRADBUF else self.y)
+        self.fkind = fk
+        # fp32 images the general-stencil row-marching kernel covers (pds_smarch.hpp: 64-column
+        # strips, 16-B groups) run through pcs_pds2d_step with K in the args; the rest through the
+        # tile kernel (pcs_pds2d_stencil_step).  PCS_STENCIL_MARCH=0: always the tile kernel.
+        self.march = False
+        a = None
+        if dtype == torch.float32 and os.environ.get('PCS_STENCIL_MARCH', '1') != '0':
+            a = L.PdsArgs()
+            a.dtype, a.fkind, a.hkind, a.gkind = L.PCS_F32, fk, spec['hkind'], spec['gkind']
+            a.n0, a.n1, a.row0, a.rows = n0, n1, 0, n0
+            a.kkind, a.edge = spec['kkind'], int(spec['edge'])
+            a.w0, a.w1 = spec['weights']
+            a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+            a.step0, a.step1 = spec['steps']
+            a.seg_a, a.seg_b = spec['seg']
+            a.x, a.xn = self.X[0].data_ptr(), self.X[1].data_ptr()
+            a.z, a.zn = self.Z[0].data_ptr(), self.Z[1].data_ptr()
+            a.partials = a.x  # placeholder for the support query (never written)
+            if fk == L.PCS_F_DENOISE:
+                a.y = gsrc.data_ptr()
+            elif fk == L.PCS_F_GRADBUF:
+                a.gbuf = gsrc.data_ptr()
+                # separable PSF: grad F = N x - Conv^T y (the in-plane normal-operator kernel into the
+                # gradient buffer, then the march step), Conv^T y formed once here in fp64
+                sep = self.conv.separable(rtol=2e-7)
+                if sep is not None and sep[2] <= 7:
+                    t0, t1, half = sep
+                    self.taps = [torch.as_tensor(t).to(device=dev, dtype=dtype) for t in (t0, t1)]
+                    self.cty = self.conv._adj(-O.to_dev(spec['shift'], torch.float64)).to(dtype).contiguous()
+                    a.fkind, a.half, a.y = L.PCS_F_SEPCONV, half, self.y.data_ptr()
+                    a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
+                    a.cty = self.cty.data_ptr()
+                    if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
+                        a.fkind, a.cty = fk, None
+                    else:
+                        fk = self.fkind = L.PCS_F_SEPCONV
+            if self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1:
+                self.march = True
+            else:
+                a = None
+                fk = self.fkind = spec['fkind']
+        if a is None:
+            a = L.StencilArgs()
+            a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+            a.kkind, a.hkind, a.gkind, a.edge = spec['kkind'], spec['hkind'], spec['gkind'], int(spec['edge'])
+            a.n0, a.n1 = n0, n1
+            a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+            a.step0, a.step1 = spec['steps']
+            a.w0, a.w1 = spec['weights']
+            a.seg_a, a.seg_b = spec['seg']
+            a.fkind = fk
+            if gsrc is not None:
+                a.g = gsrc.data_ptr()
         self.args = a
-        self.nblocks = int(self.lib.pcs_pds2d_stencil_nblocks(ctypes.byref(a)))
+        nb_fn = self.lib.pcs_pds2d_nblocks if self.march else self.lib.pcs_pds2d_stencil_nblocks
+        ws_fn = self.lib.pcs_pds2d_ws_bytes if self.march else self.lib.pcs_pds2d_stencil_ws_bytes
+        self.nblocks = int(nb_fn(ctypes.byref(a)))
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
         a.partials = self.partials.data_ptr()
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
         self.fused_finalize = True
-        self.ws = torch.zeros(int(self.lib.pcs_pds2d_stencil_ws_bytes(ctypes.byref(a))) // 8 + 2,
-                              dtype=torch.float64, device=dev)
+        self.ws = torch.zeros(int(ws_fn(ctypes.byref(a))) // 8 + 2, dtype=torch.float64, device=dev)
         a.ws = self.ws.data_ptr()
         self.graph = None
         self.hist = None
@@ -543,8 +587,33 @@ class PDS2DStencilEngine(PDS2DEngine):
         self.persistent = False
         self.bar = None
 
+    def time_iteration_kernels(self, n):
+        """As PDS2DEngine's; the normal-operator march (separable PSF, SEPCONV here) is one
+        pcs_pds2d_step call holding two launches (N x into the gradient buffer, the step), timed as
+        'step' together and 'conv_nx' alone."""
+        res = PDS2DEngine.time_iteration_kernels(self, n)
+        if self.fkind == L.PCS_F_SEPCONV:
+            a, lib = self.args, self.lib
+            ev = []
+            for i in range(min(n, 50)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                L.check(lib.pcs_conv2d_sep_ata_planes(a.dtype, L.ptr(self.X[i % 2]), L.ptr(self.Gb), 1, a.n0, a.n1,
+                                                      L.ptr(self.taps[0]), 2 * a.half + 1, a.half,
+                                                      L.ptr(self.taps[1]), 2 * a.half + 1, a.half, L.stream()),
+                        'pcs_conv2d_sep_ata_planes')
+                e1.record()
+                ev.append((e0, e1))
+            torch.cuda.synchronize()
+            res['conv_nx'] = float(np.median([s.elapsed_time(e) for s, e in ev]))
+        return res
+
     def _step_call(self, st):
+        if self.march:
+            return PDS2DEngine._step_call(self, st)
         L.check(self.lib.pcs_pds2d_stencil_step(ctypes.byref(self.args), st), 'pcs_pds2d_stencil_step')
 
     def _run_call(self, n):
+        if self.march:
+            return PDS2DEngine._run_call(self, n)
         L.check(self.lib.pcs_pds2d_stencil_run(ctypes.byref(self.args), int(n), L.stream()), 'pcs_pds2d_stencil_run')

@@ -508,7 +508,8 @@ class PDS3DEngine:
         try:
             with torch.cuda.graph(g):
                 self._chunk()
-        except RuntimeError:
+        except Exception:  # noqa: BLE001 -- torch's capture errors and the ABI's HipError alike: the
+            # flag all-gather below must run on every rank, or the others block in RCCL
             ok, g = False, None
             self._pending_ex = self._pending_ag = None  # handles of the aborted capture
             torch.cuda.synchronize()
@@ -523,19 +524,21 @@ class PDS3DEngine:
         return ok
 
     def advance(self, k):
-        """Enqueue k iterations (k a multiple of the chunk when graphs are used)."""
-        if self.use_graph and self.world > 1 and not self._tuned and self.banded and self.overlap and k >= 7:
-            self._autotune()  # eager, before the capture; then back to parity 0 for the graph
-            if self._p == 1:
+        """Enqueue exactly k iterations: the schedule trial's (the first call with k >= 7 on a
+        banded multi-GPU engine), then whole captured chunks from buffer parity 0, then eager
+        iterations (a parity fix before the replays, the remainder after them)."""
+        if not self._tuned and self.banded and self.overlap and k >= 7:
+            k -= self._autotune()  # eager, before any capture
+            self._drain()
+        if k > 0 and self.use_graph and (self.graph is not None or self._capture()):
+            if self._p == 1:  # the captured chunk starts from buffers 0
                 self.iteration(1)
                 self._p = 0
-            self._drain()
-        if self.use_graph and (self.graph is not None or self._capture()):
+                k -= 1
+                self._drain()
             for _ in range(k // self.chunk):
                 self.graph.replay()
-            return
-        if not self._tuned and self.banded and self.overlap and k >= 7:
-            k -= self._autotune()
+            k %= self.chunk
         for _ in range(k):
             self.iteration(self._p)
             self._p ^= 1

@@ -550,7 +550,8 @@ class SlabPDS2D:
             try:
                 with torch.cuda.graph(g):
                     L.check(self.lib.pcs_slab2d_run(plan, c, 0, L.stream()), 'pcs_slab2d_run')
-            except RuntimeError:
+            except Exception:  # noqa: BLE001 -- torch's capture errors and HipError alike: every rank
+                # must reach the flag all-gather below, or the others block in RCCL
                 ok, g = False, None
                 torch.cuda.synchronize()
             if self.world > 1:

@@ -5,7 +5,7 @@ last strip, several row segments with a short last one, both tap tiers (3, 7) an
 than their tier, L1 / L21, every prox_G kind, non-unit gradient steps.
 
 Tolerance: relative L2 of x and z <= 5e-5 after 12 iterations (fp32 against fp64, as the golden
-fp32 cases), diagnostics to 2e-2 relative, iteration counts exact.
+fp32 cases), diagnostics to 1e-3 relative, iteration counts exact.
 """
 
 import numpy as np
@@ -24,16 +24,17 @@ def _problem(shape, psf_len, hname, gname, steps, seed):
     n0, n1 = shape
     N = n0 * n1
     xs = OR.phantom(shape, seed=seed)
-    if psf_len == 0:  # denoising: no operator in F
+    if np.isscalar(psf_len) and psf_len == 0:  # denoising: no operator in F
         psf = None
-    elif psf_len < 0:  # non-separable (rank 2) -|psf_len| x -|psf_len| PSF: gradient-buffer path
+    elif np.isscalar(psf_len) and psf_len < 0:  # non-separable (rank 2) -|psf_len| x -|psf_len| PSF: gradient-buffer path
         q = -psf_len
         psf = rng.uniform(0.0, 1.0, (q, q))
         psf /= psf.sum()
-    else:
-        r = np.arange(psf_len) - psf_len // 2
-        t0 = np.exp(-0.5 * (r / 1.7) ** 2)
-        t1 = np.exp(-0.5 * (r / 2.3) ** 2)
+    else:  # separable: one length for both axes, or (l0, l1) (even lengths: the reference's K//2 - 1 offset)
+        l0, l1 = (psf_len, psf_len) if np.isscalar(psf_len) else psf_len
+        r0, r1 = np.arange(l0) - l0 // 2, np.arange(l1) - l1 // 2
+        t0 = np.exp(-0.5 * (r0 / 1.7) ** 2)
+        t1 = np.exp(-0.5 * (r1 / 2.3) ** 2)
         psf = np.outer(t0 / t0.sum(), t1 / t1.sum())
     return dict(shape=shape, N=N, psf=psf, y=xs.ravel() + 0.05 * rng.standard_normal(N), hname=hname, gname=gname,
                 steps=steps, lam=0.05)
@@ -96,6 +97,8 @@ CASES = [
     ((190, 256), 5, 'l1', '', (2.0, 0.5)),          # psf half 2 in tier 3, non-unit steps
     ((1000, 128), 15, 'l1', 'segment', (0.5, 1.0)),  # tall: many row segments, short last one
     ((1000, 4096), 15, 'l21', 'nonneg', (1.0, 1.0)),  # C3 width: 6-step tasks, 3-step last segment
+    ((300, 200), (4, 6), 'l21', '', (1.0, 1.0)),       # even lengths (offset K//2 - 1), tier 3, 4x6
+    ((261, 260), (14, 14), 'l1', 'nonneg', (1.0, 1.0)),  # even 14x14, tier 7 (N-table edge rows)
     # pds_pt.hpp
     ((300, 200), 0, 'l21', '', (1.0, 1.0)),            # denoising, partial last strip
     ((1030, 2048), 0, 'l1', 'segment', (2.0, 0.5)),    # denoising, C2 width, short last segment
@@ -116,8 +119,8 @@ def test_march_vs_oracle(case):
     assert rel(x, xr) < 5e-5, rel(x, xr)
     assert rel(z, zr) < 5e-5, rel(z, zr)
     np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float), dr['primal'],
-                               rtol=2e-2)
-    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float), dr['dual'], rtol=2e-2)
+                               rtol=1e-3)
+    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float), dr['dual'], rtol=1e-3)
 
 
 def test_march_is_the_kernel_in_use():
@@ -168,7 +171,7 @@ def test_c2_full_size_fused_vs_generic():
         np.testing.assert_allclose(df[col].to_numpy(float)[1:], dg[col].to_numpy(float)[1:], rtol=1e-3)
 
 
-SEP_CASES = [i for i, c in enumerate(CASES) if c[1] > 0]
+SEP_CASES = [i for i, c in enumerate(CASES) if not np.isscalar(c[1]) or c[1] > 0]
 
 
 @pytest.mark.parametrize('case', SEP_CASES)

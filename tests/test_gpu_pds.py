@@ -77,11 +77,13 @@ def _check(pds, c, dtype):
     assert x.dtype == dtype
     assert rel(x, c['x']) < tol, rel(x, c['x'])
     assert rel(z, c['z']) < tol, rel(z, c['z'])
-    dtol = 1e-6 if dtype == np.float64 else 2e-2
+    # fp32: 1e-3 relative, plus 1e-5 absolute for the late rows whose improvements (differences of
+    # iterates that agree to 5e-5) approach the fp32 rounding of the iterates themselves
+    dtol, atol = (1e-6, 0.0) if dtype == np.float64 else (1e-3, 1e-5)
     np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float), c['diag_primal'],
-                               rtol=dtol)
+                               rtol=dtol, atol=atol)
     np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float), c['diag_dual'],
-                               rtol=dtol)
+                               rtol=dtol, atol=atol)
     np.testing.assert_array_equal(diag['Iter'].to_numpy(), np.arange(pds.iter))
 
 

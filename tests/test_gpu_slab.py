@@ -495,3 +495,44 @@ def test_persistent_loop_matches_launches(monkeypatch, shape, thr):
     assert torch.equal(x2, x1) and torch.equal(z2, z1)
     k = 2 * n
     assert np.allclose(h2[1:k], h1[1:k], rtol=1e-5)
+
+
+def test_pds3d_capture_failure_falls_back_to_eager(monkeypatch):
+    """A library error (HipError) raised while a chunk is being captured leaves the 3-D engine on
+    eager launches (the capture outcome is agreed collectively, so every rank must get past the
+    failure): the run completes with the same iterates as an engine that never captured."""
+    from pycsou_amd import _lib as L
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    pds = build(vol3d_case(), np.float64, engine='fused')
+    spec = pds._fused_spec()
+    dt = pds._compute_dtype()
+    ref = PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    ref.use_graph = False
+    n0, x0, z0, _ = ref.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
+    eng = PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    orig = eng.iteration
+
+    def failing(p):
+        if torch.cuda.is_current_stream_capturing():
+            raise L.HipError('pcs_pds3d_step returned status -2 (injected)')
+        return orig(p)
+    monkeypatch.setattr(eng, 'iteration', failing)
+    n1, x1, z1, _ = eng.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
+    assert not eng.use_graph and eng.graph is None
+    assert n1 == n0
+    assert torch.equal(x1, x0) and torch.equal(z1, z0)
+
+
+@pytest.mark.parametrize('k', [1, 5, 8, 13])
+def test_pds3d_advance_issues_exactly_k(k):
+    """advance(k) issues exactly k iterations whatever the chunk and buffer parity (graph replays
+    of whole chunks from parity 0, eager iterations for the parity fix and the remainder)."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    pds = build(vol3d_case(), np.float64, engine='fused')
+    spec = pds._fused_spec()
+    eng = PDS3DEngine(spec, pds._compute_dtype(), pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, chunk=4)
+    eng.init_loop(100, 100, -1.0)
+    eng.advance(3)
+    eng.advance(k)
+    torch.cuda.synchronize()
+    assert eng.iterations() == 3 + k
