@@ -15,7 +15,7 @@ build/%.o: pycsou_amd/csrc/%.hip $(HDR)
 
 $(LIB): $(OBJ)
 	@mkdir -p pycsou_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ) -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib
 
 clean:
 	rm -rf build $(LIB)
@@ -26,5 +26,5 @@ clean:
 STAMP_LIB := pycsou_amd/lib/diag/libpycsou_hip.so
 stamps: $(SRC) $(HDR)
 	@mkdir -p pycsou_amd/lib/diag
-	$(HIPCC) $(FLAGS) -DPCS_STAMPS -shared -o $(STAMP_LIB) $(SRC)
+	$(HIPCC) $(FLAGS) -DPCS_STAMPS -shared -o $(STAMP_LIB) $(SRC) -L/opt/rocm/lib -lrocfft
 .PHONY: stamps

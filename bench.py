@@ -470,6 +470,43 @@ def leg_c3_cen(args, dtype, K, W):
                             'tflops': round(116 * N / (km.get('conv_nx', float('nan')) * 1e-3) / 1e12, 2)}}
 
 
+def leg_conv63(args, dtype, K, W):
+    """Convolve2D with a 63 x 63 non-separable PSF on a 4096^2 image (the reference's default
+    method='fft', pycsou/linop/conv.py:209-217, 294): one forward and one adjoint pass through the
+    FFT-domain plan (pcs_fftconv2d: pad, rocFFT R2C, spectrum product, C2R, crop), HIP events
+    around each of `reps` passes on the launch stream; the cost no longer grows with the PSF."""
+    from pycsou_amd.linop.conv import Convolve2D
+    n = args.size
+    r = np.arange(63) - 31.0
+    yy, xx = np.meshgrid(r, r, indexing='ij')
+    h = np.exp(-0.5 * ((xx * 0.8 + yy * 0.6) ** 2 / 90.0 + (yy * 0.8 - xx * 0.6) ** 2 / 20.0))
+    h /= h.sum()
+    C = Convolve2D(n * n, h, (n, n))
+    x = torch.randn(n * n, device='cuda', dtype=dtype)
+    f = C.fft(dtype)
+    out = torch.empty_like(x)
+    reps = max(10, min(K, 50))
+    st = torch.cuda.current_stream()
+    res = {}
+    for name, adj in (('forward', False), ('adjoint', True)):
+        for _ in range(3):
+            f.apply(x, adjoint=adj, out=out)
+        evs = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            f.apply(x, adjoint=adj, out=out)
+            e1.record(st)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        res[name] = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    lib_grid = int(C.fft(dtype)._lib.pcs_fftconv2d_grid(n, 63))
+    return {'workload': f'Convolve2D {n}x{n} {args.dtype}, 63x63 non-separable PSF, FFT-domain plan '
+                        f'(padded grid {lib_grid}^2, rocFFT R2C/C2R + pad / spectrum-product / crop kernels)',
+            'ms_per_pass': {k: round(v, 5) for k, v in res.items()}, 'reps': reps,
+            'direct_flop_equiv_tflops': round(2 * 63 * 63 * n * n / (res['forward'] * 1e-3) / 1e12, 1)}
+
+
 def slab_bench(n, dtype, K, W, world):
     """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
     (barrier + synchronize on both sides; the caller takes the max over ranks)."""
@@ -531,7 +568,7 @@ def main():
     ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
                     help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
-    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen',
+    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,conv63',
                     help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
                          'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K), c3_cen (C3 with the default '
                          'centered Gradient); "" skips them')
@@ -635,7 +672,7 @@ def main():
         if world == 1 and args.engine != 'slab':
             for leg in filter(None, args.legs.split(',')):
                 fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen,
-                      'c3_cen': leg_c3_cen}[leg]
+                      'c3_cen': leg_c3_cen, 'conv63': leg_conv63}[leg]
                 try:
                     out[leg] = fn(args, dtype, K, W)
                 except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own

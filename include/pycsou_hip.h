@@ -124,6 +124,22 @@ int pcs_conv2d_sep_planes(int dtype, const void* in, void* out, int64_t nplanes,
 int pcs_conv2d_sep_ata_planes(int dtype, const void* in, void* out, int64_t nplanes, int64_t n1, int64_t n2,
                               const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t stream);
 
+/* FFT-domain Convolve2D (pycsou/linop/conv.py:167-295, method='fft': scipy.signal.fftconvolve,
+ * mode 'same' at pycsou's offset), for PSFs of any size at a cost independent of the PSF:
+ *   forward out[i] = sum_j h[j] x[i + off - j] (+ beta b[i]);  adjoint out[i] = sum_j h[j] x[i - off + j]
+ * (zero boundary; kh x kw PSF h in host fp64, row-major; offsets off0 < kh, off1 < kw).  The plan
+ * holds the rocFFT R2C / C2R plans on a zero-padded P0 x P1 grid (P = pcs_fftconv2d_grid(n, k):
+ * the smallest even 2-3-5-7-smooth size >= n + k - 1, so the circular transforms are exact linear
+ * ones), their work buffer and the PSF spectrum (formed at creation; create synchronises).
+ * pcs_fftconv2d_apply: x != out, device arrays of n0*n1 (b may be NULL); stream-ordered, no
+ * allocation (graph-capturable).  One plan per (dtype, shape, PSF); not thread-safe per plan. */
+int64_t pcs_fftconv2d_grid(int64_t n, int k);
+int pcs_fftconv2d_create(int dtype, int64_t n0, int64_t n1, const double* h, int kh, int kw, int off0, int off1,
+                         void** handle);
+int pcs_fftconv2d_apply(void* handle, const void* x, void* out, int adjoint, const void* b, double beta,
+                        hipStream_t stream);
+int pcs_fftconv2d_destroy(void* handle);
+
 /* The axis-0 stage of grad F = C^T (C x - y) for a 3-D Convolve1D chain, in one pass
  * (pycsou/linop/conv.py:20-164 along axis 0, residual of core/map.py:609-610): on sub-volumes
  * of nsub planes of `plane` elements,

@@ -124,6 +124,11 @@ _SIGS = {
     'pcs_pds2d_nblocks': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_ws_bytes': (_c_i64, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_step': (_c_int, [ctypes.POINTER(PdsArgs), _vp]),
+    'pcs_fftconv2d_grid': (_c_i64, [_c_i64, _c_int]),
+    'pcs_fftconv2d_create': (_c_int, [_c_int, _c_i64, _c_i64, _pdbl, _c_int, _c_int, _c_int, _c_int,
+                                      ctypes.POINTER(_vp)]),
+    'pcs_fftconv2d_apply': (_c_int, [_vp, _vp, _vp, _c_int, _vp, _c_dbl, _vp]),
+    'pcs_fftconv2d_destroy': (_c_int, [_vp]),
     'pcs_pds2d_supported': (_c_int, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
     'pcs_pds2d_stencil_nblocks': (_c_i64, [ctypes.POINTER(StencilArgs)]),

@@ -8,6 +8,8 @@ gfx950 kernels.
 
 from numbers import Number
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -322,6 +324,36 @@ def conv2d_planned(x, dims, plan, b=None, beta=0.0, out=None):
     L.check(lib.pcs_conv2d_planned(L.dtcode(x), L.ptr(x), L.ptr(out), int(dims[0]), int(dims[1]), L.ptr(w), int(tier),
                                    L.ptr(b), float(beta), L.stream()), 'pcs_conv2d_planned')
     return out
+
+
+class FFTConv2D:
+    """An FFT-domain Convolve2D plan (pcs_fftconv2d_*: rocFFT R2C / C2R on the zero-padded grid,
+    PSF spectrum formed once) for one (dtype, image shape, PSF); freed with the object."""
+
+    def __init__(self, psf, dims, off0, off1, dtype):
+        lib = L.gpu()
+        self._lib = lib
+        h = np.ascontiguousarray(np.asarray(psf, dtype=np.float64))
+        kh, kw = h.shape
+        code = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
+        handle = ctypes.c_void_p()
+        L.check(lib.pcs_fftconv2d_create(code, int(dims[0]), int(dims[1]), h.ctypes.data_as(L._pdbl), kh, kw,
+                                         int(off0), int(off1), ctypes.byref(handle)), 'pcs_fftconv2d_create')
+        self.handle, self.dims, self.dtype = handle, tuple(dims), dtype
+
+    def apply(self, x, adjoint=False, b=None, beta=0.0, out=None):
+        """Conv x (+ beta b) or Conv^T x into a new (or the given) device vector."""
+        if x.dtype != self.dtype:
+            raise ValueError('FFTConv2D: dtype mismatch')
+        out = torch.empty_like(x) if out is None else out
+        L.check(self._lib.pcs_fftconv2d_apply(self.handle, L.ptr(x), L.ptr(out), int(bool(adjoint)), L.ptr(b),
+                                              float(beta), L.stream()), 'pcs_fftconv2d_apply')
+        return out
+
+    def __del__(self):
+        if getattr(self, 'handle', None):
+            self._lib.pcs_fftconv2d_destroy(self.handle)
+            self.handle = None
 
 
 def conv1d(x, dims, axis, taps_dev, k, off):

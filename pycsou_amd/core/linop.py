@@ -36,7 +36,7 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     within r of it, so the sum is an upper estimate of the extreme eigenvalue (the one the Ritz
     value approximates) -- PDS step sizes built from it stay inside tau sigma ||K||^2 <= 1
     (pycsou/opt/proxalgs.py:280-301) instead of exceeding it by the Ritz value's deficit."""
-    from scipy.linalg import eigh_tridiagonal
+    from scipy.linalg import eigh_tridiagonal, eigvalsh_tridiagonal
     dev = O.device()
     g = torch.Generator(device='cpu').manual_seed(seed)
     q = torch.randn(n, generator=g, dtype=torch.float64).to(dev)
@@ -63,11 +63,17 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
         bad = np.nonzero(~np.isfinite(be) | (be <= 1e-13 * scale))[0]
         k = int(bad[0]) + 1 if bad.size else j + 1  # T of size k: alphas[:k], betas[:k-1]
         if k > 1:
-            ev, S = eigh_tridiagonal(al[:k], be[:k - 1])
-            i = int(np.argmax(np.abs(ev))) if sym else k - 1
-            theta = float(abs(ev[i])) if sym else float(ev[i])
+            # the extreme eigenvalue, then its eigenvector alone (O(k) per check, not the O(k^2)
+            # of a full eigendecomposition of T)
+            i = k - 1
+            if sym:
+                ends = eigvalsh_tridiagonal(al[:k], be[:k - 1], select='i', select_range=(0, 0)), \
+                    eigvalsh_tridiagonal(al[:k], be[:k - 1], select='i', select_range=(k - 1, k - 1))
+                i = 0 if abs(ends[0][0]) > abs(ends[1][0]) else k - 1
+            ev, S = eigh_tridiagonal(al[:k], be[:k - 1], select='i', select_range=(i, i))
+            theta = float(abs(ev[0])) if sym else float(ev[0])
             # residual of the Ritz pair: the next beta times the last component of its vector
-            resid = 0.0 if bad.size else float(abs(be[k - 1] * S[-1, i]))
+            resid = 0.0 if bad.size else float(abs(be[k - 1] * S[-1, 0]))
         else:
             theta, resid = (float(abs(al[0])) if sym else float(al[0])), (0.0 if bad.size else float(abs(be[0])))
         if (bad.size or resid <= tol * abs(theta)

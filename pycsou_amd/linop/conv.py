@@ -55,6 +55,7 @@ class Convolve2DOp(LinearOperator):
         self._h = _DevCache(filt)
         self._hf = _DevCache(filt[::-1, ::-1])
         self._plans = {}
+        self._ffts = {}
 
     def plan(self, dtype, adjoint):
         """(tier, packed window) for pcs_conv2d_planned, or None (PSF wider than 31)."""
@@ -63,25 +64,32 @@ class Convolve2DOp(LinearOperator):
             self._plans[key] = O.conv2d_plan(self.filter, self.off[0], self.off[1], adjoint, dtype)
         return self._plans[key]
 
+    def fft(self, dtype):
+        """The FFT-domain plan (pcs_fftconv2d, rocFFT) used when the PSF is wider than the direct
+        correlation's tiers (> 31 taps): cost independent of the PSF size, as the reference's
+        default method='fft' (conv.py:209-217, 294)."""
+        if dtype not in self._ffts:
+            self._ffts[dtype] = O.FFTConv2D(self.filter, self.dims, self.off[0], self.off[1], dtype)
+        return self._ffts[dtype]
+
     def _apply(self, t):
         p = self.plan(t.dtype, False)
         if p is not None:
             return O.conv2d_planned(t, self.dims, p)
-        return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off)
+        return self.fft(t.dtype).apply(t)
 
     def _apply_minus(self, t, y):
-        """Conv x - y in one kernel (residual of the data-fidelity term)."""
+        """Conv x - y in one pass (residual of the data-fidelity term)."""
         p = self.plan(t.dtype, False)
         if p is not None:
             return O.conv2d_planned(t, self.dims, p, b=y, beta=-1.0)
-        return O.conv2d(t, self.dims, self._h.get(t.dtype), self.kh, self.kw, *self.off, b=y, beta=-1.0)
+        return self.fft(t.dtype).apply(t, b=y, beta=-1.0)
 
     def _adj(self, t):
         p = self.plan(t.dtype, True)
         if p is not None:
             return O.conv2d_planned(t, self.dims, p)
-        return O.conv2d(t, self.dims, self._hf.get(t.dtype), self.kh, self.kw, self.kh - 1 - self.off[0],
-                        self.kw - 1 - self.off[1])
+        return self.fft(t.dtype).apply(t, adjoint=True)
 
     def separable(self, rtol=1e-12):
         """(taps_axis0, taps_axis1, half) with centred taps of length 2*half+1 if the PSF is

@@ -239,9 +239,11 @@ class PDS2DEngine:
             else:
                 fk = L.PCS_F_GRADBUF
                 self.conv = conv
-                # device PSF copies / packed correlation plans exist before capture
+                # device PSF copies / packed correlation plans / the FFT plan exist before capture
                 conv._h.get(dtype), conv._hf.get(dtype)
                 self.plans = (conv.plan(dtype, False), conv.plan(dtype, True))
+                if self.plans[0] is None or self.plans[1] is None:
+                    conv.fft(dtype)
                 self.R = torch.empty(self.N, dtype=dtype, device=dev)
                 self.Gb = torch.empty(self.N, dtype=dtype, device=dev)
                 a.gbuf = self.Gb.data_ptr()
@@ -304,11 +306,10 @@ class PDS2DEngine:
             L.check(lib.pcs_conv2d_planned(a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(adj[1]), adj[0],
                                            None, 0.0, st), 'pcs_conv2d_planned')
             return
-        h, hf = c._h.get(self.dtype), c._hf.get(self.dtype)
-        L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.X[p]), L.ptr(self.R), n0, n1, L.ptr(h), c.kh, c.kw, c.off[0],
-                               c.off[1], L.ptr(self.y), -1.0, st), 'pcs_conv2d')
-        L.check(lib.pcs_conv2d(a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(hf), c.kh, c.kw,
-                               c.kh - 1 - c.off[0], c.kw - 1 - c.off[1], None, 0.0, st), 'pcs_conv2d')
+        # wider PSFs: the FFT-domain plan (rocFFT; cost independent of the PSF size)
+        f = c.fft(self.dtype)
+        f.apply(self.X[p], b=self.y, beta=-1.0, out=self.R)
+        f.apply(self.R, adjoint=True, out=self.Gb)
 
     def _chunk(self, hist):
         for i in range(self.chunk):
@@ -513,6 +514,8 @@ class PDS2DStencilEngine(PDS2DEngine):
             conv = self.conv = spec['conv']
             conv._h.get(dtype), conv._hf.get(dtype)
             self.plans = (conv.plan(dtype, False), conv.plan(dtype, True))
+            if self.plans[0] is None or self.plans[1] is None:
+                conv.fft(dtype)  # created before any capture
             self.R = torch.empty(N, dtype=dtype, device=dev)
             self.Gb = torch.empty(N, dtype=dtype, device=dev)
         gsrc = None if fk == L.PCS_F_NULL else (self.Gb if fk == L.PCS_F_GRADBUF else self.y)
