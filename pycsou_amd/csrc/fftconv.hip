@@ -11,6 +11,8 @@
 // ordered with no allocation or host synchronisation, so it is hipGraph-capturable.
 #include <rocfft/rocfft.h>
 
+#include <stdlib.h>
+
 #include <new>
 
 #include "common.hpp"
@@ -30,8 +32,11 @@ struct FftConv {
   void* hf = nullptr;    // complex P0 x H1: spectrum of the padded PSF / (P0 P1)
 };
 
-// smallest even n' >= n whose prime factors are 2, 3, 5, 7 (rocFFT radices)
+// smallest even n' >= n whose prime factors are 2, 3, 5, 7 (rocFFT radices); PCS_FFT_GRID=<m>
+// (diagnostics) forces m when m >= n
 static int64_t fft_size(int64_t n) {
+  const char* e = getenv("PCS_FFT_GRID");
+  if (e && atoll(e) >= n) return atoll(e);
   for (int64_t m = n + (n & 1);; m += 2) {
     int64_t r = m;
     for (int p : {2, 3, 5, 7})

@@ -16,8 +16,10 @@
 //         issue the next step's z loads
 //   U     rows [a+1, a+16]: K^T z from the z ring, x_t, u -> u ring, x' -> HBM.  Every item also
 //         computes a fifth column: c0 - 1 (group 0) or c + 4 (the rest; group 15's is c0 + 64),
-//         the u columns K u of the strip's edge columns reaches; issue the next step's x, y|g
+//         the u columns K u of the strip's edge columns reaches
 //   Z     rows [a, a+16): K u from the u ring, fenchel prox, relaxation, z' -> HBM
+// The next step's x and y|g load at the top of the step too, into the second of two register
+// sets (the march is unrolled by two steps), so every load has a whole step to land.
 // z and u live in 32-row LDS rings (row r in slot r & 31; columns [c0 - 4, c0 + 68)), so every
 // z row is read from HBM once per strip, every u row computed once; x and y|g are read once.
 // HBM traffic per pixel: x, y|g, z (D components) in; x', z' out -- (3 + 2 D) words when F reads
@@ -33,6 +35,18 @@
 #include "pds_march.hpp"
 
 namespace pcs {
+
+// cache-policy bits of the x' / z' stores: 16 = sc1 (written through, not left dirty in L2):
+// 2048^2 30.5-30.6 against 31.9-32.0 us per iteration back to back with plain stores, nt (2)
+// 30.9 / 34.7 (tools/sm_probe.py, profiles/r3_sm_store_policy.jsonl); diagnostics builds override
+#ifndef PCS_SM_SAUX
+#define PCS_SM_SAUX 16
+#endif
+
+// wave priority 3 while a step's loads issue (as pds_pt.hpp); PCS_SM_PRIO=0 (diagnostics) drops it
+#ifndef PCS_SM_PRIO
+#define PCS_SM_PRIO 1
+#endif
 
 enum { SK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED (2 components) or the Laplacian (1)
 // FK beyond the public kinds: grad F = g - b with g = N x = Conv^T Conv x from a buffer (the in-plane
@@ -186,8 +200,10 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     lo_z[k] = 4 * g;
     co_z[k] = col_off(c0 - 4 + 4 * g, n1);
   }
-  G4<T> zr[D][KZ], xr, gr, br;
-  T xe = T(0), ge = T(0), be = T(0);
+  // x, y|g (and b) of the U items in two register sets: the set of step k + 1 loads at the top of
+  // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index)
+  G4<T> zr[D][KZ], xr[2], gr[2], br[2];
+  T xe[2] = {T(0), T(0)}, ge[2] = {T(0), T(0)}, be[2] = {T(0), T(0)};
   // z rows [a + ZHI - 15, a + ZHI] (rows below rmin read as 0)
   auto loads_z = [&](int a, int rmin) {
 #pragma unroll
@@ -207,27 +223,29 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
           st4(ZR + d * RING * WZ + ((a + M::ZHI - 15 + rr_z[k]) & 31) * WZ + lo_z[k], zr[d][k]);
   };
   // x and y|g of U row a + 1 + ui: the group and the fifth column
-  auto loads_x = [&](int a, int rmin) {
+  auto loads_x = [&](auto pb, int a, int rmin) {
+    constexpr int PB = decltype(pb)::value;
     const int r = a + 1 + ui;
     const uint32_t ro = r < rmin ? kOOB : vx.row_off(r);
-    xr = bload4(vx.r, ro + co_c);
-    xe = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vx.r, (int)(ro + co_e), 0, 0));
+    xr[PB] = bload4(vx.r, ro + co_c);
+    xe[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vx.r, (int)(ro + co_e), 0, 0));
     if constexpr (FK != PCS_F_NULL) {
       const uint32_t rg = r < rmin ? kOOB : vg.row_off(r);
-      gr = bload4(vg.r, rg + co_c);
-      ge = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vg.r, (int)(rg + co_e), 0, 0));
+      gr[PB] = bload4(vg.r, rg + co_c);
+      ge[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vg.r, (int)(rg + co_e), 0, 0));
     }
     if constexpr (FK == SM_F_NB) {
       const uint32_t rb = r < rmin ? kOOB : vb.row_off(r);
-      br = bload4(vb.r, rb + co_c);
-      be = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(rb + co_e), 0, 0));
+      br[PB] = bload4(vb.r, rb + co_c);
+      be[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(rb + co_e), 0, 0));
     }
   };
 
   // ---- U: x_t, u on row lr = a + 1 + ui, columns c .. c + 3 and ce; x' on own cells
   // RI (std::true_type / false_type): every row of the step lies >= 2 rows inside the image
-  auto uphase = [&](auto ri, int a) {
+  auto uphase = [&](auto ri, auto pb, int a) {
     constexpr bool RI = decltype(ri)::value;
+    constexpr int PB = decltype(pb)::value;
     const int lr = a + 1 + ui, gr_ = s.row0 + lr;
     const T* Z0 = ZR;
     const T* Z1 = ZR + (D - 1) * RING * WZ;  // the axis-1 component (the Laplacian's only one)
@@ -270,11 +288,11 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
         kt = T(0) + sw_d1_adj<KK, RI>(w0, gr_, n0, P.inv_step0, edge);
         kt += sw_d1_adj<KK, CI>(w1, i1, n1, P.inv_step1, edge);
       }
-      const T xv = m < 4 ? xr.v[m] : xe;
+      const T xv = m < 4 ? xr[PB].v[m] : xe[PB];
       T gf = T(0);
-      if constexpr (FK == PCS_F_DENOISE) gf = xv - (m < 4 ? gr.v[m] : ge);  // (2 (x + (-y))) 0.5, exact
-      else if constexpr (FK == PCS_F_GRADBUF) gf = m < 4 ? gr.v[m] : ge;
-      else if constexpr (FK == SM_F_NB) gf = (m < 4 ? gr.v[m] : ge) - (m < 4 ? br.v[m] : be);
+      if constexpr (FK == PCS_F_DENOISE) gf = xv - (m < 4 ? gr[PB].v[m] : ge[PB]);  // (2 (x + (-y))) 0.5, exact
+      else if constexpr (FK == PCS_F_GRADBUF) gf = m < 4 ? gr[PB].v[m] : ge[PB];
+      else if constexpr (FK == SM_F_NB) gf = (m < 4 ? gr[PB].v[m] : ge[PB]) - (m < 4 ? br[PB].v[m] : be[PB]);
       const T xt = prox_g((xv - P.tau * gf) - P.tau * kt, gk, P.seg_a, P.seg_b);
       const bool in = rrow && (m < 4 ? cin : ce_in);
       const T u = in ? (T(2) * xt - xv) : T(0);
@@ -296,7 +314,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     T* urow = UR + (lr & 31) * WZ;
     st4(urow + lc, uo);
     if (ext_st) urow[lce] = ue;
-    bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
+    bstore4<PCS_SM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
   };
 
   // ---- Z: z' on row lr = a + ui, columns c .. c + 3
@@ -365,38 +383,48 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     }
     const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_c;
 #pragma unroll
-    for (int d = 0; d < D; ++d) bstore4(rzn[d], off, o[d]);
+    for (int d = 0; d < D; ++d) bstore4<PCS_SM_SAUX>(rzn[d], off, o[d]);
   };
 
   // prologue: u on rows [s0 - UPRO, s0] (a pseudo-step at a = s0 - TS whose loads skip the rows
   // it does not need), x' on row s0
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
   const int nsteps = (s1 - s0 + TS - 1) / TS;
   loads_z(s0 - TS, s0 - M::ZPRO);
-  loads_x(s0 - TS, s0 - M::UPRO);
+  loads_x(P0{}, s0 - TS, s0 - M::UPRO);
   lds_barrier();  // rings zeroed
   land_z(s0 - TS);
-  if (nsteps > 0) loads_z(s0, -(1 << 30));
+  if (nsteps > 0) {
+    loads_z(s0, -(1 << 30));
+    loads_x(P1{}, s0, -(1 << 30));
+  }
   lds_barrier();
-  uphase(std::false_type{}, s0 - TS);
-  if (nsteps > 0) loads_x(s0, -(1 << 30));
-  for (int k = 0; k < nsteps; ++k) {
+  uphase(std::false_type{}, P0{}, s0 - TS);
+  // step k reads register set PB = (k + 1) & 1 and loads the other one for step k + 1
+  auto step = [&](auto pb, int k) {
+    constexpr int PB = decltype(pb)::value;
     const int a = s0 + k * TS;
     // rows [a, a + 16] at >= 2 rows from both image edges (uniform)
     const bool ri = s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0;
     lds_barrier();  // the previous step's Z phase is done with the rings
     land_z(a);
-    __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU (as pds_pt.hpp)
-    if (k + 1 < nsteps) loads_z(a + TS, -(1 << 30));
-    __builtin_amdgcn_s_setprio(0);
+    if (PCS_SM_PRIO) __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
+    if (k + 1 < nsteps) {
+      loads_z(a + TS, -(1 << 30));
+      loads_x(std::integral_constant<int, 1 - PB>{}, a + TS, -(1 << 30));
+    }
+    if (PCS_SM_PRIO) __builtin_amdgcn_s_setprio(0);
     lds_barrier();
-    if (ri) uphase(std::true_type{}, a);
-    else uphase(std::false_type{}, a);
-    __builtin_amdgcn_s_setprio(3);
-    if (k + 1 < nsteps) loads_x(a + TS, -(1 << 30));
-    __builtin_amdgcn_s_setprio(0);
+    if (ri) uphase(std::true_type{}, pb, a);
+    else uphase(std::false_type{}, pb, a);
     lds_barrier();
     if (ri) zphase(std::true_type{}, a);
     else zphase(std::false_type{}, a);
+  };
+  for (int k = 0; k < nsteps; k += 2) {
+    step(P1{}, k);
+    if (k + 1 < nsteps) step(P0{}, k + 1);
   }
 #undef PCS_WAVE_ON
 #undef PCS_ITEM

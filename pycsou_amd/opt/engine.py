@@ -37,6 +37,24 @@ from ..linop.diff import GradientOp, LaplacianOp
 NATIVE_MIN_PIXELS = int(os.environ.get('PCS_NATIVE_MIN_PIXELS', 1 << 20))
 
 
+HIST_CHUNK = 4096  # iterations of device history allocated at first; doubled as the loop goes on
+
+
+def grow_hist(hist, ctrl, need_iters, total):
+    """Device history with room for `need_iters` iterations (at most `total`): `hist` itself, or a
+    copy twice as long with the loop control's length updated (stream-ordered after every
+    iteration already enqueued).  A max_iter of 1e9 with accuracy_threshold doing the stopping
+    must not allocate 2 * max_iter doubles up front."""
+    have = (hist.numel() - 2) // 2
+    if need_iters + 1 <= have or have >= total:
+        return hist
+    cap = min(total, max(2 * have, need_iters + 1))
+    new = torch.full((2 * cap + 2,), float('nan'), dtype=torch.float64, device=hist.device)
+    new[:hist.numel()].copy_(hist)
+    ctrl.view(torch.int32)[5].fill_(int(new.numel()))  # Ctrl.hist_len (csrc/pds_ctrl.hpp)
+    return new
+
+
 def _half_loss_data(F):
     """If F is (1/2) * SquaredL2Norm.shifter(s) return s (the shift = -data), else None."""
     if (isinstance(F, DiffMapComp) and isinstance(F.map1, HomothetyMap) and F.map1.cst == 0.5
@@ -440,26 +458,30 @@ class PDS2DEngine:
         return float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
     def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        max_iter, min_iter = int(max_iter), int(min_iter)
         total = max(min_iter, max_iter) + 1
-        hist_len = 2 * total + 2
+        hist_len = 2 * min(total, max(HIST_CHUNK, 2 * self.chunk)) + 2
         if self.hist is None or self.hist.numel() < hist_len:
             # the history buffer is captured by pointer: (re)capture when it grows
             self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
             self.graph = None
-        hist = self.hist
-        hist.fill_(float('nan'))
-        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
-                                        int(has_dual), int(hist.numel()), L.stream()), 'pcs_ctrl_init2')
+        self.hist.fill_(float('nan'))
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), min_iter, max_iter, float(accuracy_threshold),
+                                        int(has_dual), int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
         n_chunks = -(-total // self.chunk)
         if self.use_graph or self.native:
-            if self.graph is None and not self.native:
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._chunk(hist)
-                self.graph = g
             pending = []
             for k in range(n_chunks):
+                grown = grow_hist(self.hist, self.ctrl, (k + 1) * self.chunk + 1, total)
+                if grown is not self.hist:
+                    self.hist, self.graph = grown, None
+                hist = self.hist
+                if self.graph is None and not self.native:
+                    torch.cuda.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._chunk(hist)
+                    self.graph = g
                 if self.native:
                     self._chunk_native(hist)
                 else:
@@ -474,9 +496,11 @@ class PDS2DEngine:
                         break
         else:
             for k in range(n_chunks):
-                self._chunk(hist)
+                self.hist = grow_hist(self.hist, self.ctrl, (k + 1) * self.chunk + 1, total)
+                self._chunk(self.hist)
                 if int(self.ctrl.view(torch.int32)[1].item()) != 0:
                     break
+        hist = self.hist
         torch.cuda.synchronize()
         if self.persistent and self.barrier_timed_out():
             # a persistent chunk's grid barrier gave up: x / z hold a mix of iterations and the

@@ -40,7 +40,7 @@ from ..func.penalty import L1Norm, L21Norm
 from ..linop.conv import Convolve1DOp
 from ..linop.diff import GradientOp
 from ..parallel.slab import SlabLayout
-from .engine import _half_loss_data
+from .engine import HIST_CHUNK, _half_loss_data, grow_hist
 
 
 def conv_chain(C, shape):
@@ -482,8 +482,10 @@ class PDS3DEngine:
 
     # ---- loops
     def init_loop(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        max_iter, min_iter = int(max_iter), int(min_iter)
         total = max(min_iter, max_iter) + 1
-        hist_len = 2 * total + 2
+        self._total, self._issued = total, 0
+        hist_len = 2 * min(total, max(HIST_CHUNK, 2 * self.chunk)) + 2
         if self.hist is None or self.hist.numel() < hist_len:
             self.hist = torch.empty(hist_len, dtype=torch.float64, device=self.X[0].device)
             self.graph = None
@@ -527,6 +529,10 @@ class PDS3DEngine:
         """Enqueue exactly k iterations: the schedule trial's (the first call with k >= 7 on a
         banded multi-GPU engine), then whole captured chunks from buffer parity 0, then eager
         iterations (a parity fix before the replays, the remainder after them)."""
+        grown = grow_hist(self.hist, self.ctrl, self._issued + k + 1, self._total)
+        if grown is not self.hist:  # the captured chunk holds the history pointer: recapture
+            self.hist, self.graph = grown, None
+        self._issued += k
         if not self._tuned and self.banded and self.overlap and k >= 7:
             k -= self._autotune()  # eager, before any capture
             self._drain()

@@ -78,25 +78,51 @@ class _DeviceLoop:
     iterations behind (no blocking .item() per iteration); iterations issued past the stop
     are discarded by the caller, which keeps the last ``lag + 2`` states."""
 
+    # the device history starts at this many iterations and doubles as the loop issues more (a
+    # max_iter of 1e9 with accuracy_threshold doing the stopping must not allocate 16 GB up front)
+    HIST_CHUNK = 4096
+
     def __init__(self, max_iter, min_iter, thr, has_dual, device, lag=3):
         from .. import _lib as L
         self.L, self.lib = L, L.gpu()
+        max_iter, min_iter = int(max_iter), int(min_iter)
         self.total = max(min_iter, max_iter) + 1
-        self.hist = torch.full((2 * self.total + 2,), float('nan'), dtype=torch.float64, device=device)
+        cap = min(self.total, self.HIST_CHUNK)
+        self.hist = torch.full((2 * cap + 2,), float('nan'), dtype=torch.float64, device=device)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=device)
         self.sums = torch.zeros(4, dtype=torch.float64, device=device)
-        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(thr), int(has_dual),
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), min_iter, max_iter, float(thr), int(has_dual),
                                         int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
         self.has_dual, self.lag = has_dual, lag
         self.pending = []  # (pinned host copy of (it, stopped), event)
         self.final = None
+        self.issued = 0
+
+    def _grow(self):
+        """Before iteration `issued` is recorded: make room for its history row (and the stop test
+        of the next), doubling the device buffer and its length in the control block -- both
+        stream-ordered after every finalize already enqueued."""
+        need = 2 * (self.issued + 2) + 2
+        if need <= self.hist.numel():
+            return
+        cap = min(self.total, max(2 * ((self.hist.numel() - 2) // 2), self.issued + 2))
+        new = torch.full((2 * cap + 2,), float('nan'), dtype=torch.float64, device=self.hist.device)
+        new[:self.hist.numel()].copy_(self.hist)
+        self.hist = new
+        self.ctrl.view(torch.int32)[5].fill_(int(new.numel()))  # Ctrl.hist_len (pds_ctrl.hpp)
 
     def record(self, x_old, x, z_old=None, z=None):
         """Enqueue this iteration's sums + finalize and an async read-back of the control."""
-        L = self.L
         O.rel_sums(x_old, x, self.sums[0:2])
         if self.has_dual:
             O.rel_sums(z_old, z, self.sums[2:4])
+        self.finalize()
+
+    def finalize(self):
+        """The loop control of the iteration whose sums are in ``sums``, and its read-back."""
+        L = self.L
+        self._grow()
+        self.issued += 1
         L.check(self.lib.pcs_pds_finalize(L.ptr(self.sums), L.ptr(self.ctrl), L.ptr(self.hist), L.stream()),
                 'pcs_pds_finalize')
         host = torch.empty(2, dtype=torch.int32, pin_memory=True)
@@ -104,6 +130,20 @@ class _DeviceLoop:
         ev = torch.cuda.Event()
         ev.record()
         self.pending.append((host, ev))
+
+    def stream_rows(self, every, show):
+        """``verbose``: show(k, row) for every resolved iteration k with k % every == 0, while the
+        loop runs (solver.py:69-71 prints inside the loop) -- at most ``lag`` iterations late."""
+        self._every, self._show, self._shown = int(every), show, 0
+
+    def _emit(self, done):
+        show = getattr(self, '_show', None)
+        if show is None:
+            return
+        for k in range(self._shown, done):
+            if k % self._every == 0:
+                show(k, self.hist[2 * k:2 * k + 2].cpu().numpy())
+        self._shown = max(self._shown, done)
 
     def poll(self, drain=False):
         """Resolve finished read-backs in order; returns the iteration count once the device
@@ -114,6 +154,7 @@ class _DeviceLoop:
                 break
             ev.synchronize()
             self.pending.pop(0)
+            self._emit(int(host[0]))
             if int(host[1]) != 0:
                 self.final = int(host[0])
         return self.final
@@ -293,6 +334,11 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         self.init_iterand_dev = dict(state)
         loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, bool(self._H),
                            state['primal_variable'].device)
+        if self.verbose is not None:
+            def show(k, h):
+                self._rows = [[k, h[0], h[1]] if self._H else [k, h[0]]]
+                self.print_diagnostics()
+            loop.stream_rows(self.verbose, show)
         states = {-1: state}
         i, n = 0, None
         while n is None:
@@ -309,14 +355,6 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         self.iter = n
         h = loop.rows(n)
         self._rows = [[k, h[k, 0], h[k, 1]] if self._H else [k, h[k, 0]] for k in range(n)]
-        if self.verbose is not None:
-            # the reference prints row ``iter`` every ``verbose`` iterations inside its loop
-            # (solver.py:69-71); here the rows come from the device history after the loop
-            rows = self._rows
-            for row in rows[::self.verbose]:
-                self._rows = [row]
-                self.print_diagnostics()
-            self._rows = rows
         self._state = states[n - 1]
         self.converged = True
         cols = ['Iter', 'Relative Improvement (primal variable)']
@@ -434,6 +472,11 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         dtype = self._compute_dtype()
         x0 = O.to_dev(self.x0, dtype)
         loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, False, x0.device)
+        if self.verbose is not None:
+            def show(k, h):
+                self._rows = [[k, h[0]]]
+                self.print_diagnostics()
+            loop.stream_rows(self.verbose, show)
         states = {-1: (x0, torch.zeros_like(x0), 1)}
         i, n = 0, None
         while n is None:
@@ -444,13 +487,7 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
             new = self._update_dev(states[i - 1], sums_out=loop.sums[0:2])
             if self._sums is None:
                 O.rel_sums(states[i - 1][0], new[0], loop.sums[0:2])
-            loop.L.check(loop.lib.pcs_pds_finalize(loop.L.ptr(loop.sums), loop.L.ptr(loop.ctrl),
-                                                   loop.L.ptr(loop.hist), loop.L.stream()), 'pcs_pds_finalize')
-            host = torch.empty(2, dtype=torch.int32, pin_memory=True)
-            host.copy_(loop.ctrl.view(torch.int32)[:2], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            loop.pending.append((host, ev))
+            loop.finalize()
             states[i] = new
             states.pop(i - loop.lag - 3, None)
             i += 1
@@ -458,12 +495,6 @@ class AcceleratedProximalGradientDescent(GenericIterativeAlgorithm):
         self.iter = n
         h = loop.rows(n)
         self._rows = [[k, h[k, 0]] for k in range(n)]
-        if self.verbose is not None:
-            rows = self._rows
-            for row in rows[::self.verbose]:
-                self._rows = [row]
-                self.print_diagnostics()
-            self._rows = rows
         self._state = states[n - 1]
         self.converged = True
         self.diagnostics = _frame(['Iter', 'Relative Improvement'], self._rows)

@@ -356,12 +356,11 @@ class SlabPDS2D:
             a.y = self.y.data_ptr()
         if (fk == L.PCS_F_SEPCONV and dtype == torch.float32 and half <= 7
                 and os.environ.get('PCS_NMARCH', '1') != '0'):
-            # normal-operator march kernel (as PDS2DEngine): Conv^T y of the global image in fp64,
-            # this rank's window of it (own rows + the y halo)
+            # normal-operator march kernel (as PDS2DEngine): Conv^T y in fp64 on this rank's window
+            # only (own rows + the y halo), from the y rows within the PSF's reach of it -- exact,
+            # since the sub-image's zero boundary falls where the image's does or beyond the reach
             self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
-            cty = spec['conv']._adj(-O.to_dev(spec['shift'], torch.float64)).to(dtype)
-            self.cty = lay.window(cty, hy).contiguous()
-            del cty
+            self.cty = self._cty_window(spec, hy).to(dtype).contiguous()
             a.cty, a.ntaps = self.cty.data_ptr(), self.ntaps.data_ptr()
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
@@ -391,6 +390,24 @@ class SlabPDS2D:
         gc = int(os.environ.get('PCS_SLAB_GRAPH', '32' if world > 1 else '0') or 0)
         self.graph_chunk = (gc + gc % 2) if self.native and gc > 0 else 0
         self._graph = None
+
+    def _cty_window(self, spec, h):
+        """Rows [row0 - h, row0 + rows + h) of Conv^T y (fp64, zeros outside the image), computed on
+        the sub-image of y rows within the PSF's reach of that window (never the global image)."""
+        from ..linop.conv import Convolve2DOp
+        conv, n0, n1 = spec['conv'], self.n0, self.n1
+        reach = max(conv.kh, conv.kw)
+        wlo, whi = max(0, self.row0 - h - reach), min(n0, self.row0 + self.rows + h + reach)
+        shift = spec['shift']
+        ys = shift.reshape(n0, n1)[wlo:whi] if isinstance(shift, torch.Tensor) else \
+            np.asarray(shift).reshape(n0, n1)[wlo:whi]
+        yw = -O.to_dev(ys, torch.float64)
+        ctw = Convolve2DOp(n1 * (whi - wlo), conv.filter, (whi - wlo, n1))._adj(yw)
+        out = torch.zeros((self.rows + 2 * h) * n1, dtype=torch.float64, device=ctw.device)
+        lo, hi = max(0, self.row0 - h), min(n0, self.row0 + self.rows + h)
+        d = lo - (self.row0 - h)
+        out[d * n1:(d + hi - lo) * n1] = ctw[(lo - wlo) * n1:(hi - wlo) * n1]
+        return out
 
     @classmethod
     def from_pds(cls, pds, comm, rank=None, world=None, chunk=16, native='auto', overlap=True):

@@ -10,4 +10,4 @@ for f in pycsou_amd/csrc/*.hip; do
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p || exit 1; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o pycsou_amd/lib/var/$name/libpycsou_hip.so $o/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o pycsou_amd/lib/var/$name/libpycsou_hip.so $o/*.o -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib
