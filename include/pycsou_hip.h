@@ -37,7 +37,7 @@ enum { PCS_H_L1 = 0, PCS_H_L21 = 1 };
 /* G functional kinds in the fused step */
 enum { PCS_G_NULL = 0, PCS_G_NONNEG = 1, PCS_G_SEGMENT = 2 };
 /* F kinds in the fused step */
-enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3 };
+enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3, PCS_F_CONV2D = 4 };
 /* finite-difference K of the fused 2-D steps */
 enum { PCS_K_GRAD_FORWARD = 0, PCS_K_GRAD_BACKWARD = 1, PCS_K_GRAD_CENTERED = 2, PCS_K_LAPLACIAN = 3 };
 
@@ -264,14 +264,26 @@ typedef struct {
    * = Conv^T (Conv x - y) as four (2 tier + 1)-tap passes. */
   const void* cty;
   const void* ntaps;
-  /* K (appended in ABI 1.1; all zero = the forward Gradient of the fields above).  kkind
+  /* K (appended in ABI 2; all zero = the forward Gradient of the fields above).  kkind
    * PCS_K_GRAD_{FORWARD,BACKWARD,CENTERED}: K = Gradient(kind, edge, step0/1), z = [D0 x; D1 x];
    * PCS_K_LAPLACIAN: K = w0 D2_0 + w1 D2_1 (Laplacian(weights, step, edge), z has rows*n1
    * elements, H = lam*L1).  Non-forward K: the general-stencil row-marching kernel (fp32, F = NULL /
-   * DENOISE / GRADBUF, n1 % 4 == 0, 16-B aligned, at least two 64-column strips; slabs need halo
-   * rows x >= 2, y >= 2, z >= 4); PCS_EUNSUPPORTED otherwise (pcs_pds2d_stencil_step covers the rest). */
+   * DENOISE / GRADBUF / SEPCONV with cty (grad F = N x - cty, N x into gbuf first) / CONV2D,
+   * n1 % 4 == 0, 16-B aligned, at least two 64-column strips; slabs need halo rows x >= 2,
+   * y >= 2, z >= 4); PCS_EUNSUPPORTED otherwise (pcs_pds2d_stencil_step covers the rest). */
   int kkind, edge;
   double w0, w1;
+  /* fkind PCS_F_CONV2D (ABI 3): a general (non-separable) Convolve2D in F, grad F = Conv^T (Conv x - y)
+   * by two pcs_conv2d_planned passes (conv_fwd / conv_adj: packed windows of tier conv_tier) over
+   * the stored rows of x clipped to the image, into rbuf (the residual) and gbuf, inside this call
+   * before the step (any K).  y, rbuf and gbuf share x's layout (halo_y == halo_x); a slab needs
+   * halo_x >= conv_tier + 1 so that the rows the step reads are exact.  With fkind PCS_F_SEPCONV,
+   * cty and a non-forward K, N x goes to gbuf the same way (halo_y == halo_x, halo_x >= 2 + 2 tier).
+   * Neither runs banded (pcs_pds2d_step_bands: PCS_EUNSUPPORTED). */
+  const void* conv_fwd;
+  const void* conv_adj;
+  int conv_tier, pad3;
+  void* rbuf;
 } pcs_pds2d_args;
 /* 1 if pcs_pds2d_step runs these arguments (0: PCS_EUNSUPPORTED / invalid). */
 int pcs_pds2d_supported(const pcs_pds2d_args* a);

@@ -20,7 +20,7 @@ PCS_H_L1, PCS_H_L21 = 0, 1
 PCS_K_GRAD_FORWARD, PCS_K_GRAD_BACKWARD, PCS_K_GRAD_CENTERED, PCS_K_LAPLACIAN = 0, 1, 2, 3
 PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
 PCS_APGD_G_L1 = 3
-PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF = 0, 1, 2, 3
+PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF, PCS_F_CONV2D = 0, 1, 2, 3, 4
 KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
 
 _c_int, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -40,7 +40,8 @@ class PdsArgs(ctypes.Structure):
                 ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp),
                 ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64),
                 ('cty', _vp), ('ntaps', _vp),
-                ('kkind', _c_int), ('edge', _c_int), ('w0', _c_dbl), ('w1', _c_dbl)]
+                ('kkind', _c_int), ('edge', _c_int), ('w0', _c_dbl), ('w1', _c_dbl),
+                ('conv_fwd', _vp), ('conv_adj', _vp), ('conv_tier', _c_int), ('pad3', _c_int), ('rbuf', _vp)]
 
 
 class StencilArgs(ctypes.Structure):

@@ -431,11 +431,19 @@ static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
 // F = (1/2)||Conv x - y||^2, Conv separable, with a non-forward K: grad F = N x - Conv^T y, N x by the
 // in-plane normal-operator kernel into gbuf (pcs_conv2d_sep_ata_planes on the whole image: two
 // composite-tap passes), then the march step reads gbuf and cty -- whole images only
+// local rows [lo, hi) of the stored window (halo h) clipped to the image
+static void window_rows(const pcs_pds2d_args* a, int h, int64_t* lo, int64_t* hi) {
+  *lo = -h > -a->row0 ? -h : -a->row0;
+  *hi = a->rows + h < a->n0 - a->row0 ? a->rows + h : a->n0 - a->row0;
+}
+
 static bool sm_normal(const pcs_pds2d_args* a) {
-  if (a->fkind != PCS_F_SEPCONV || !a->cty || !a->gbuf || !aligned16(a->cty) || a->rows != a->n0) return false;
+  if (a->fkind != PCS_F_SEPCONV || !a->cty || !a->gbuf || !aligned16(a->cty) || a->halo_y != a->halo_x) return false;
   if (a->half < 0 || a->half > 7 || !a->taps0 || !a->taps1) return false;
-  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 0, a->n0, a->n1, a->taps0, 2 * a->half + 1, a->half,
-                                   a->taps1, 2 * a->half + 1, a->half, nullptr) == PCS_OK;
+  int64_t lo, hi;
+  window_rows(a, a->halo_x, &lo, &hi);
+  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1, a->taps0,
+                                   2 * a->half + 1, a->half, a->taps1, 2 * a->half + 1, a->half, nullptr) == PCS_OK;
 }
 
 static bool use_smarch(const pcs_pds2d_args* a) {
@@ -491,10 +499,15 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 template <int KK>
 static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  if (a->fkind == PCS_F_SEPCONV) {  // N x -> gbuf, then the step with grad F = gbuf - cty
-    if (KK == PCS_FORWARD || rb.ra0 != 0 || rb.rb1 != a->rows) return PCS_EUNSUPPORTED;
-    const int rc = pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 1, a->n0, a->n1, a->taps0, 2 * a->half + 1,
-                                             a->half, a->taps1, 2 * a->half + 1, a->half, st);
+  if (a->fkind == PCS_F_SEPCONV) {  // N x -> gbuf on the stored rows (clipped to the image), then the
+    // step with grad F = gbuf - cty; whole slabs only (the N x pass runs once per iteration)
+    if (KK == PCS_FORWARD || rb.ra0 != 0 || rb.rb0 != a->rows) return PCS_EUNSUPPORTED;
+    int64_t lo, hi;
+    window_rows(a, a->halo_x, &lo, &hi);
+    const int64_t off = (lo + a->halo_x) * a->n1;
+    const int rc = pcs_conv2d_sep_ata_planes(PCS_F32, (const float*)a->x + off, (float*)const_cast<void*>(a->gbuf) + off,
+                                             1, hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half, a->taps1,
+                                             2 * a->half + 1, a->half, st);
     if (rc != PCS_OK) return rc;
     return launch_smarch<KK, SM_F_NB>(a, rb, st);
   }
@@ -564,7 +577,7 @@ static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb) {
 }
 
 static int needed_halo_x(int fkind, int half) {
-  if (fkind != PCS_F_SEPCONV) return 1;
+  if (fkind != PCS_F_SEPCONV) return 1;  // CONV2D: checked against conv_tier in check_args
   const int t = tier_for(half);
   return t < 0 ? -1 : 2 * t + 1;
 }
@@ -582,7 +595,33 @@ int pcs_pds2d_ntaps_len(int half) {
   return (t == 3 || t == 7) ? 64 + 32 * t : -1;
 }
 
+// a CONV2D call = its two correlation passes + the GRADBUF step of these arguments
+static pcs_pds2d_args step_args(const pcs_pds2d_args* a) {
+  pcs_pds2d_args b = *a;
+  if (b.fkind == PCS_F_CONV2D) b.fkind = PCS_F_GRADBUF;
+  return b;
+}
+
+// grad F = Conv^T (Conv x - y) of a general Convolve2D over the stored rows clipped to the image:
+// r = Conv x - y -> rbuf, g = Conv^T r -> gbuf (pcs_conv2d_planned; y, rbuf, gbuf in x's layout)
+static int conv2d_prepass(const pcs_pds2d_args* a, hipStream_t st) {
+  int64_t lo, hi;
+  window_rows(a, a->halo_x, &lo, &hi);
+  const int64_t off = (lo + a->halo_x) * a->n1 * (a->dtype == PCS_F32 ? 4 : 8);
+  const char* xb = (const char*)a->x + off;
+  const char* yb = (const char*)a->y + off;
+  char* rb = (char*)a->rbuf + off;
+  char* gb = (char*)const_cast<void*>(a->gbuf) + off;
+  int rc = pcs_conv2d_planned(a->dtype, xb, rb, hi - lo, a->n1, a->conv_fwd, a->conv_tier, yb, -1.0, st);
+  if (rc == PCS_OK) rc = pcs_conv2d_planned(a->dtype, rb, gb, hi - lo, a->n1, a->conv_adj, a->conv_tier, nullptr, 0.0, st);
+  return rc;
+}
+
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
+  if (a && a->fkind == PCS_F_CONV2D) {
+    const pcs_pds2d_args b = step_args(a);
+    return pcs_pds2d_nblocks(&b);
+  }
   if (!a || a->rows < 1 || a->n1 < 1) return -1;
   if (use_smarch(a) || a->kkind != PCS_K_GRAD_FORWARD) return bands_nblocks(a, full_bands(a));
   if (use_march(a) || use_pt(a)) return bands_nblocks(a, full_bands(a));
@@ -603,6 +642,7 @@ static int check_args(const pcs_pds2d_args* a) {
        (a->n_pre > 0 && !a->pre_partials)))
     return PCS_EINVAL;
   if (a->n0 < 1 || a->n1 < 1 || a->rows < 1 || a->row0 < 0 || a->row0 + a->rows > a->n0) return PCS_EINVAL;
+  const bool multi = a->rows < a->n0;
   if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return PCS_EINVAL;
   if (a->gkind < PCS_G_NULL || a->gkind > PCS_G_SEGMENT) return PCS_EINVAL;
   if (!(a->sigma > 0) || !(a->step0 != 0) || !(a->step1 != 0)) return PCS_EINVAL;
@@ -611,12 +651,18 @@ static int check_args(const pcs_pds2d_args* a) {
   if (a->kkind != PCS_K_GRAD_FORWARD && a->rows < a->n0 &&
       (a->halo_x < 2 || a->halo_z < 4 || (a->fkind != PCS_F_NULL && a->halo_y < 2)))
     return PCS_EINVAL;
+  if (a->fkind == PCS_F_CONV2D) {  // two planned correlations over the stored window, then GRADBUF
+    if (!a->conv_fwd || !a->conv_adj || !a->rbuf || !a->gbuf || !a->y || a->halo_y != a->halo_x) return PCS_EINVAL;
+    if (a->conv_tier < 3 || (a->conv_tier & 1) || (multi && a->halo_x < a->conv_tier + 1)) return PCS_EINVAL;
+  }
+  if (a->fkind == PCS_F_SEPCONV && a->kkind != PCS_K_GRAD_FORWARD && multi &&
+      (a->halo_y != a->halo_x || a->halo_x < 2 + 2 * tier_for(a->half)))
+    return PCS_EINVAL;
   if ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_SEPCONV) && !a->y) return PCS_EINVAL;
   if (a->fkind == PCS_F_GRADBUF && !a->gbuf) return PCS_EINVAL;
   if (a->fkind == PCS_F_SEPCONV && (!a->taps0 || !a->taps1 || a->half < 0)) return PCS_EINVAL;
   const int hxn = needed_halo_x(a->fkind, a->half);
   if (hxn < 0) return PCS_EUNSUPPORTED;
-  const bool multi = a->rows < a->n0;
   if (multi && (a->halo_x < hxn || a->halo_z < 1 ||
                 ((a->fkind == PCS_F_SEPCONV) && a->halo_y < tier_for(a->half) + 1) ||
                 ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_GRADBUF) && a->halo_y < 1)))
@@ -638,20 +684,31 @@ int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int6
   const int rc = check_args(a);
   if (rc != PCS_OK) return rc;
   if (a->hist || !bands_ok(a, ra0, rb0, ra1, rb1)) return PCS_EINVAL;
+  if (a->fkind == PCS_F_CONV2D) return PCS_EUNSUPPORTED;  // its correlation passes run once per iteration
   if (!(use_smarch(a) || (a->kkind == PCS_K_GRAD_FORWARD && (use_march(a) || use_pt(a))))) return PCS_EUNSUPPORTED;
   return pds2d_bands(a, RowBands{ra0, rb0, ra1, rb1}, st);
 }
 
 int pcs_pds2d_supported(const pcs_pds2d_args* a) {
   if (check_args(a) != PCS_OK) return 0;
+  if (a->fkind == PCS_F_CONV2D) {
+    const pcs_pds2d_args b = step_args(a);
+    return pcs_pds2d_supported(&b);
+  }
   if (a->kkind != PCS_K_GRAD_FORWARD) return use_smarch(a) ? 1 : 0;
   if (use_smarch(a) || use_march(a) || use_pt(a)) return 1;
   return (a->dtype == PCS_F32 || a->dtype == PCS_F64) && (a->fkind != PCS_F_SEPCONV || tier_for(a->half) > 0) ? 1 : 0;
 }
 
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {
-  const int rc = check_args(a);
+  int rc = check_args(a);
   if (rc != PCS_OK) return rc;
+  if (a->fkind == PCS_F_CONV2D) {
+    rc = conv2d_prepass(a, st);
+    if (rc != PCS_OK) return rc;
+    const pcs_pds2d_args b = step_args(a);
+    return pcs_pds2d_step(&b, st);
+  }
   if (a->dtype == PCS_F32) return pds2d<float>(a, st);
   if (a->dtype == PCS_F64) return pds2d<double>(a, st);
   return PCS_EINVAL;

@@ -316,6 +316,9 @@ class SlabPDS2D:
         self.lay = lay = SlabLayout(n0, n1, rank, world)
         self.row0, self.rows = lay.row0, lay.rows
         fk = spec['fkind']
+        kk = spec.get('kkind', L.PCS_K_GRAD_FORWARD)
+        nc = spec.get('ncomp', 2)
+        self.ncomp = nc
         a = L.PdsArgs()
         a.dtype = L.PCS_F32 if dtype == torch.float32 else L.PCS_F64
         a.hkind, a.gkind = spec['hkind'], spec['gkind']
@@ -323,45 +326,76 @@ class SlabPDS2D:
         a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
         a.step0, a.step1 = spec['steps']
         a.seg_a, a.seg_b = spec['seg']
+        a.kkind, a.edge = kk, int(spec.get('edge', True))
+        a.w0, a.w1 = spec.get('weights', (1.0, 1.0))
         dev = torch.device('cuda', torch.cuda.current_device())
-        half = 0
-        if fk == L.PCS_F_SEPCONV:
-            sep = spec['conv'].separable(rtol=2e-7 if dtype == torch.float32 else 1e-13)
-            if sep is None:
-                raise ValueError('row-slab PDS needs a separable (rank-1) PSF; non-separable convolutions run '
-                                 'on one GPU (PDS2DEngine)')
-            t0, t1, half = sep
-            self.taps = [torch.as_tensor(t0).to(device=dev, dtype=dtype),
-                         torch.as_tensor(t1).to(device=dev, dtype=dtype)]
-            a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
-            a.half = half
+        fwd = kk == L.PCS_K_GRAD_FORWARD
+        half, mode = 0, 'pointwise'
+        conv = spec.get('conv')
+        if fk in (L.PCS_F_SEPCONV, L.PCS_F_GRADBUF) and conv is not None:
+            sep = conv.separable(rtol=2e-7 if dtype == torch.float32 else 1e-13)
+            if sep is not None and (fwd or (dtype == torch.float32 and sep[2] <= 7)):
+                # forward K: the (normal-operator) march kernels; other K: N x by the in-plane
+                # normal-operator pass into a buffer, then the general-stencil march step
+                mode = 'sep' if fwd else 'sep_normal'
+                t0, t1, half = sep
+                self.taps = [torch.as_tensor(t0).to(device=dev, dtype=dtype),
+                             torch.as_tensor(t1).to(device=dev, dtype=dtype)]
+                a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
+                a.half = half
+                fk = L.PCS_F_SEPCONV
+            else:
+                # general (non-separable) PSF: grad F = Conv^T (Conv x - y) by two packed-plan
+                # correlations over the stored rows inside the step call (PCS_F_CONV2D)
+                mode = 'conv2d'
+                plans = (conv.plan(dtype, False), conv.plan(dtype, True))
+                if plans[0] is None or plans[1] is None:
+                    raise ValueError('row-slab PDS: PSF wider than the direct correlation tiers (31 taps)')
+                self.plans = plans
+                a.conv_fwd, a.conv_adj, a.conv_tier = plans[0][1].data_ptr(), plans[1][1].data_ptr(), plans[0][0]
+                fk = L.PCS_F_CONV2D
         elif fk not in (L.PCS_F_NULL, L.PCS_F_DENOISE):
             raise ValueError(f'row-slab PDS does not support fkind {fk}')
         a.fkind = fk
-        self.fkind = fk
-        # halo depths: the tier the kernel uses for `half` sets its reach
-        hx = int(self.lib.pcs_pds2d_halo_x(half)) if fk == L.PCS_F_SEPCONV else 1
-        hy = (hx - 1) // 2 + 1 if fk == L.PCS_F_SEPCONV else 1
-        hz = 1
+        self.fkind, self.mode = fk, mode
+        # halo depths: the reach of the step (and of the gradient passes it runs on the stored rows)
+        if mode == 'sep':
+            hx = int(self.lib.pcs_pds2d_halo_x(half))
+            hy = (hx - 1) // 2 + 1
+        elif mode == 'sep_normal':
+            hx = hy = 2 + 2 * (3 if half <= 3 else 7)
+        elif mode == 'conv2d':
+            hx = hy = max(a.conv_tier + 1, 1 if fwd else 2)
+        else:
+            hx, hy = (1, 1) if fwd else (2, 2)
+        hz = 1 if fwd else 4
         if world > 1 and self.rows < max(hx, hy, hz):
-            raise ValueError(f'slab of {self.rows} rows is thinner than its halo ({hx} rows)')
+            raise ValueError(f'slab of {self.rows} rows is thinner than its halo ({max(hx, hy, hz)} rows)')
         self.hx, self.hy, self.hz = hx, hy, hz
         a.halo_x, a.halo_y, a.halo_z = hx, hy, hz
         N = n0 * n1
         self.X = [lay.window(O.to_dev(x0, dtype), hx) for _ in range(2)]
         z0d = O.to_dev(z0, dtype)
-        self.Z = [torch.cat([lay.window(z0d[:N], hz), lay.window(z0d[N:], hz)]) for _ in range(2)]
-        if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV):
+        self.Z = [torch.cat([lay.window(z0d[c * N:(c + 1) * N], hz) for c in range(nc)]) for _ in range(2)]
+        if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV, L.PCS_F_CONV2D):
             self.y = lay.window(-O.to_dev(spec['shift'], dtype), hy)  # y = -shift, exactly
             a.y = self.y.data_ptr()
-        if (fk == L.PCS_F_SEPCONV and dtype == torch.float32 and half <= 7
-                and os.environ.get('PCS_NMARCH', '1') != '0'):
-            # normal-operator march kernel (as PDS2DEngine): Conv^T y in fp64 on this rank's window
-            # only (own rows + the y halo), from the y rows within the PSF's reach of it -- exact,
-            # since the sub-image's zero boundary falls where the image's does or beyond the reach
-            self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+        if mode in ('sep_normal', 'conv2d'):
+            self.Gb = torch.zeros_like(self.X[0])  # grad F on the stored rows (x's layout)
+            a.gbuf = self.Gb.data_ptr()
+        if mode == 'conv2d':
+            self.R = torch.zeros_like(self.X[0])
+            a.rbuf = self.R.data_ptr()
+        if mode == 'sep_normal' or (mode == 'sep' and dtype == torch.float32 and half <= 7
+                                    and os.environ.get('PCS_NMARCH', '1') != '0'):
+            # Conv^T y in fp64 on this rank's window only (own rows + the y halo), from the y rows
+            # within the PSF's reach of it -- exact, since the sub-image's zero boundary falls where
+            # the image's does or beyond the reach
+            if mode == 'sep':
+                self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+                a.ntaps = self.ntaps.data_ptr()
             self.cty = self._cty_window(spec, hy).to(dtype).contiguous()
-            a.cty, a.ntaps = self.cty.data_ptr(), self.ntaps.data_ptr()
+            a.cty = self.cty.data_ptr()
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
         a.partials = self.partials.data_ptr()
@@ -371,7 +405,7 @@ class SlabPDS2D:
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
         self.args = [self._args_for(a, p) for p in (0, 1)]
-        self.halos = [lay.halo_pairs([(self.X[q], hx, 0), (self.Z[q], hz, 0), (self.Z[q], hz, 1)]) for q in (0, 1)]
+        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c) for c in range(nc)]) for q in (0, 1)]
         self.hist = None
         self.chunk = max(1, int(chunk))
         # native loop (pcs_slab2d_run): one C call per chunk instead of five Python-issued
@@ -381,7 +415,9 @@ class SlabPDS2D:
         elif native and world > 1 and (comm is None or comm.native() is None):
             raise ValueError('native slab loop needs an RCCL (nccl backend) process group')
         self.native = bool(native)
-        self.overlap = bool(overlap)
+        # the gradient passes of 'conv2d' / 'sep_normal' run once per iteration over the whole slab:
+        # no banded (overlapped) schedule for them
+        self.overlap = bool(overlap) and mode in ('pointwise', 'sep')
         self._plan = None
         self._plan_key = None
         # multi-GPU native loop: chunks of 32 iterations replayed from a hipGraph (kernels, events
@@ -627,7 +663,7 @@ class SlabPDS2D:
         n = self.iterations()
         q = n % 2
         x = self.lay.rows_view(self.X[q], self.hx, 0, self.rows).clone()
-        z = torch.cat([self.lay.rows_view(self.Z[q], self.hz, 0, self.rows, c) for c in (0, 1)])
+        z = torch.cat([self.lay.rows_view(self.Z[q], self.hz, 0, self.rows, c) for c in range(self.ncomp)])
         h = self.hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
         return n, x, z, h
 

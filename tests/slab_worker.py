@@ -13,6 +13,52 @@ import torch
 import torch.distributed as dist
 
 
+# synthetic slab problems (no golden: the single-GPU fused engine is the reference):
+# name -> (shape, K kind, H, PSF, dtype)
+SYNTH = {
+    'cen_denoise_f32': ((300, 200), 'centered', 'l21', None, np.float32),
+    'lap_denoise_f32': ((260, 192), 'lap', 'l1', None, np.float32),
+    'bwd_denoise_f32': ((150, 132), 'backward', 'l1', None, np.float32),
+    'nonsep_fwd_f64': ((120, 96), 'forward', 'l21', 'nonsep9', np.float64),
+    'nonsep_fwd_f32': ((140, 256), 'forward', 'l1', 'nonsep9', np.float32),
+    'nonsep_cen_f32': ((200, 192), 'centered', 'l21', 'nonsep9', np.float32),
+    'sep_cen_f32': ((240, 256), 'centered', 'l21', 'sep15', np.float32),
+}
+
+
+def synth_problem(name, niter=16):
+    """A PDS of the SYNTH table through the public API (fixed iteration count)."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L1Norm, L21Norm
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient, Laplacian
+    from pycsou_amd.opt.proxalgs import PDS
+    shape, kind, hname, psf, dtype = SYNTH[name]
+    N = shape[0] * shape[1]
+    rng = np.random.default_rng(11)
+    y = rng.uniform(0, 1, N).astype(dtype)
+    F = (1 / 2) * SquaredL2Loss(dim=N, data=y)
+    if psf is not None:
+        if psf == 'sep15':
+            r = np.arange(15) - 7.0
+            g = np.exp(-0.5 * (r / 2.0) ** 2)
+            h = np.outer(g, g)
+        else:  # 9 x 9, rank > 1
+            h = rng.uniform(0, 1, (9, 9))
+        C = Convolve2D(N, h / h.sum(), shape)
+        C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
+        F = F * C
+    if kind == 'lap':
+        K, hdim = Laplacian(shape, edge=True), N
+        K.lipschitz_cst = K.diff_lipschitz_cst = 8.0
+    else:
+        K, hdim = Gradient(shape, kind=kind), 2 * N
+        K.lipschitz_cst = K.diff_lipschitz_cst = np.sqrt(8.0)
+    H = 0.05 * (L21Norm(dim=hdim, groups=np.tile(np.arange(N), 2)) if hname == 'l21' else L1Norm(dim=hdim))
+    return PDS(dim=N, F=F, H=H, K=K, x0=np.zeros(N, dtype), z0=np.zeros(hdim, dtype), max_iter=niter - 1,
+               min_iter=niter - 1, accuracy_threshold=0.0, verbose=None, engine='fused')
+
+
 def main(name, outdir):
     torch.cuda.set_device(0)
     dist.init_process_group('gloo')
@@ -31,8 +77,7 @@ def main(name, outdir):
         n, x, z, h = eng.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
         xg = gather_rows(x, eng.n0, eng.plane, comm.world, comm.rank, comm)
     else:
-        c = pds_case(name)
-        pds = build(c, np.float64, engine='fused')
+        pds = synth_problem(name) if name in SYNTH else build(pds_case(name), np.float64, engine='fused')
         eng = SlabPDS2D.from_pds(pds, comm, chunk=4)
         n, x, z, h = eng.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
         xg = gather_rows(x, eng.n0, eng.n1, comm.world, comm.rank, comm)
