@@ -127,10 +127,11 @@ int pcs_conv2d_sep_ata_planes(int dtype, const void* in, void* out, int64_t npla
 /* FFT-domain Convolve2D (pycsou/linop/conv.py:167-295, method='fft': scipy.signal.fftconvolve,
  * mode 'same' at pycsou's offset), for PSFs of any size at a cost independent of the PSF:
  *   forward out[i] = sum_j h[j] x[i + off - j] (+ beta b[i]);  adjoint out[i] = sum_j h[j] x[i - off + j]
- * (zero boundary; kh x kw PSF h in host fp64, row-major; offsets off0 < kh, off1 < kw).  The plan
- * holds the rocFFT R2C / C2R plans on a zero-padded P0 x P1 grid (P = pcs_fftconv2d_grid(n, k):
- * the smallest even 2-3-5-7-smooth size >= n + k - 1, so the circular transforms are exact linear
- * ones), their work buffer and the PSF spectrum (formed at creation; create synchronises).
+ * (zero boundary; kh x kw PSF h in host fp64, row-major; offsets off0 < kh, off1 < kw).  Overlap-add
+ * over blocks of at most 2048 x 2048 samples: the plan holds batched rocFFT R2C / C2R plans on a
+ * zero-padded P0 x P1 grid per block (P = pcs_fftconv2d_grid(n, k): the smallest even 2-3-5-7-smooth
+ * size >= block + k - 1, so the circular transforms are exact linear ones), their work buffer and
+ * the PSF spectrum (formed at creation; create synchronises).
  * pcs_fftconv2d_apply: x != out, device arrays of n0*n1 (b may be NULL); stream-ordered, no
  * allocation (graph-capturable).  One plan per (dtype, shape, PSF); not thread-safe per plan. */
 int64_t pcs_fftconv2d_grid(int64_t n, int k);

@@ -442,8 +442,10 @@ static bool sm_normal(const pcs_pds2d_args* a) {
   if (a->half < 0 || a->half > 7 || !a->taps0 || !a->taps1) return false;
   int64_t lo, hi;
   window_rows(a, a->halo_x, &lo, &hi);
-  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1, a->taps0,
-                                   2 * a->half + 1, a->half, a->taps1, 2 * a->half + 1, a->half, nullptr) == PCS_OK;
+  // shape / tap validation only (nplanes 0): any non-null input will do before x is bound
+  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x ? a->x : a->cty, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1,
+                                   a->taps0, 2 * a->half + 1, a->half, a->taps1, 2 * a->half + 1, a->half,
+                                   nullptr) == PCS_OK;
 }
 
 static bool use_smarch(const pcs_pds2d_args* a) {
@@ -653,7 +655,7 @@ static int check_args(const pcs_pds2d_args* a) {
     return PCS_EINVAL;
   if (a->fkind == PCS_F_CONV2D) {  // two planned correlations over the stored window, then GRADBUF
     if (!a->conv_fwd || !a->conv_adj || !a->rbuf || !a->gbuf || !a->y || a->halo_y != a->halo_x) return PCS_EINVAL;
-    if (a->conv_tier < 3 || (a->conv_tier & 1) || (multi && a->halo_x < a->conv_tier + 1)) return PCS_EINVAL;
+    if (a->conv_tier < 3 || !(a->conv_tier & 1) || (multi && a->halo_x < a->conv_tier + 1)) return PCS_EINVAL;
   }
   if (a->fkind == PCS_F_SEPCONV && a->kkind != PCS_K_GRAD_FORWARD && multi &&
       (a->halo_y != a->halo_x || a->halo_x < 2 + 2 * tier_for(a->half)))

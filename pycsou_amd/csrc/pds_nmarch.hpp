@@ -41,6 +41,12 @@
 #ifndef PCS_NM_EDGE
 #define PCS_NM_EDGE 1
 #endif
+// cache-policy bits of the x' / z' stores (16 = sc1: written through, not left dirty in L2)
+// C2 2048^2: 31.4 against 32.3 us per iteration, C3 4096^2: 112.7 against 113.9 us (two alternating
+// reps each, profiles/r3_store_policy_ab.txt)
+#ifndef PCS_NM_SAUX
+#define PCS_NM_SAUX 16
+#endif
 
 #include "pds_march.hpp"
 
@@ -355,7 +361,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     }
     T* urow = U + slot * WU + 4 * ug;
     st4(urow, uo);
-    bstore4(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+    bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
     if (ug == GG - 1) {  // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0)
       const T* q0 = p0 + 4;
       T g4 = T(0);
@@ -418,8 +424,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       part[3] += (double)sz;
     }
     const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_u;
-    bstore4(rzn0, off, o0);
-    bstore4(rzn1, off, o1);
+    bstore4<PCS_NM_SAUX>(rzn0, off, o0);
+    bstore4<PCS_NM_SAUX>(rzn1, off, o1);
   };
 
   // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0

@@ -24,6 +24,12 @@ namespace pcs {
 #ifndef PCS_PT_PRIO
 #define PCS_PT_PRIO 1
 #endif
+// cache-policy bits of the per-launch kernel's x' / z' stores (16 = sc1: written through, not left dirty in L2)
+// C2 2048^2: 31.4 against 32.3 us per iteration, C3 4096^2: 112.7 against 113.9 us (two alternating
+// reps each, profiles/r3_store_policy_ab.txt)
+#ifndef PCS_PT_SAUX
+#define PCS_PT_SAUX 16
+#endif
 
 struct PtGeom {
   static constexpr int TW = 64, TS = 16, UROWS = TS + 1, WG = TW + 4, GG = WG / 4;
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
   int s0, s1;
   band_rows(bd, seg, s0, s1);
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  if (!stopped) pt_task<FK, HK>(x, xn, z, zn, gsrc, s, P, gk, s0, s1, strip * PtGeom::TW, sm, part);
+  if (!stopped) pt_task<FK, HK, PCS_PT_SAUX>(x, xn, z, zn, gsrc, s, P, gk, s0, s1, strip * PtGeom::TW, sm, part);
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);

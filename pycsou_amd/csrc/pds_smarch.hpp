@@ -54,9 +54,13 @@ enum { SK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED (2 compon
 enum { SM_F_NB = 16 };
 
 // ---- the stencils on a 5-sample window w[k] = a[i + k - 2] along one axis (stencil.hpp order);
-// INT: the sample is known to lie >= 2 samples inside the axis (no edge rule applies)
+// INT: the sample is known to lie >= 2 samples inside the axis (no edge rule applies).  No FMA
+// contraction inside them: the interior and the edge instantiations of a sample give the same bits,
+// so a pixel's result does not depend on which row step it falls in (slabs are bitwise equal to
+// the whole image)
 template <int KIND, bool INT>
 __device__ __forceinline__ float sw_d1_fwd(const float (&w)[5], int i, int n, float ih, int edge) {
+#pragma clang fp contract(off)
   if constexpr (KIND == PCS_FORWARD) {
     const float c = (w[3] - w[2]) * ih;
     return (INT || i < n - 1) ? c : 0.f;
@@ -72,6 +76,7 @@ __device__ __forceinline__ float sw_d1_fwd(const float (&w)[5], int i, int n, fl
 }
 template <int KIND, bool INT>
 __device__ __forceinline__ float sw_d1_adj(const float (&w)[5], int i, int n, float ih, int edge) {
+#pragma clang fp contract(off)
   float acc = 0.f;
   if constexpr (KIND == PCS_FORWARD) {
     if (INT || i < n - 1) acc -= w[2] * ih;
@@ -93,6 +98,7 @@ __device__ __forceinline__ float sw_d1_adj(const float (&w)[5], int i, int n, fl
 }
 template <bool INT>
 __device__ __forceinline__ float sw_d2_fwd(const float (&w)[5], int i, int n, float ih2, int edge) {
+#pragma clang fp contract(off)
   const float c = (w[3] - 2.f * w[2] + w[1]) * ih2;
   if constexpr (INT) return c;
   const float e = (i == 0) ? (w[2] - 2.f * w[3] + w[4]) * ih2 : (w[0] - 2.f * w[1] + w[2]) * ih2;
@@ -100,6 +106,7 @@ __device__ __forceinline__ float sw_d2_fwd(const float (&w)[5], int i, int n, fl
 }
 template <bool INT>
 __device__ __forceinline__ float sw_d2_adj(const float (&w)[5], int i, int n, float ih2, int edge) {
+#pragma clang fp contract(off)
   float acc = 0.f;
   if (INT || i <= n - 3) acc += w[3] * ih2;
   if (INT || (i >= 1 && i <= n - 2)) acc -= (2.f * w[2]) * ih2;
