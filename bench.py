@@ -190,10 +190,11 @@ def cpu_baseline(n, iters):
                       f'in {dt:.1f} s on 1 host core'}
 
 
-def build_volume(n, dtype, seed=0):
+def build_volume(n, dtype, seed=0, kind='forward'):
     """C5 through the public API: a piecewise-constant n^3 phantom blurred by a 15-tap
     Gaussian (sigma 2) along each axis (Convolve1D x 3), y = h*x + 0.01 N(0,1), PDS with the
-    3-D forward Gradient and 0.05 L21Norm (isotropic TV)."""
+    3-D Gradient (kind='forward', or the reference's default 'centered') and 0.05 L21Norm
+    (isotropic TV)."""
     from pycsou_amd.func.loss import SquaredL2Loss
     from pycsou_amd.func.penalty import L21Norm
     from pycsou_amd.linop.conv import Convolve1D
@@ -219,21 +220,24 @@ def build_volume(n, dtype, seed=0):
     g = torch.Generator(device='cuda').manual_seed(seed + 1)
     y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
     del xs
-    K = Gradient(shape=shape, kind='forward')
-    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(3 * 4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    K = Gradient(shape=shape, kind=kind)
+    if kind == 'forward':
+        K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(3 * 4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2))
+    else:  # Schur bound per axis: rows sum to <= 2, columns to <= 1.5 -> ||D|| <= sqrt(3), ||K|| <= 3
+        K.lipschitz_cst = K.diff_lipschitz_cst = 3.0
     F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
     H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
     return PDS(dim=N, F=F, H=H, K=K, x0=torch.zeros(N, dtype=dtype, device='cuda'),
                z0=torch.zeros(3 * N, dtype=dtype, device='cuda'), verbose=None)
 
 
-def volume_bench(n, dtype, K, W, world, rank):
+def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
     """C4 / C5: the whole n^3 volume plane-slab sharded over `world` ranks; K timed iterations
     (barrier + synchronize on both sides, max over ranks)."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     from pycsou_amd.parallel import DistComm
     t0 = time.perf_counter()
-    pds = build_volume(n, dtype)
+    pds = build_volume(n, dtype, kind=kind)
     spec = pds._fused_spec()
     assert spec is not None and spec.get('ndim') == 3, 'C5 problem must take the fused 3-D engine'
     comm = DistComm() if world > 1 else None
@@ -268,7 +272,8 @@ def volume_bench(n, dtype, K, W, world, rank):
     alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
     halo = 0 if world == 1 else (eng.hx + 3 * eng.hz) * eng.plane * elem
     res = {'workload': f'{"C5" if elem == 8 else "C4"} 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
-                       f'(Convolve1D x3), 3-D Gradient(kind=forward), 0.05*L21Norm, PDS3DEngine, '
+                       f'(Convolve1D x3), 3-D Gradient(kind={kind}), 0.05*L21Norm, PDS3DEngine '
+                       f'({"k_pds3d" if kind == "forward" else "k_pds3d_gen"} update), '
                        f'{world} plane slab(s) (strong scaling: whole volume at every N)',
            'it_per_s': round(1e3 / ms, 3), 'ms_per_iter': round(ms, 4), 'steps': K, 'warmup': W,
            'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
@@ -507,6 +512,74 @@ def leg_conv63(args, dtype, K, W):
             'direct_flop_equiv_tflops': round(2 * 63 * 63 * n * n / (res['forward'] * 1e-3) / 1e12, 1)}
 
 
+def _kernel_launches(fn):
+    """GPU kernels launched while fn() runs (torch.profiler's device activity), or None when the
+    profiler cannot see the device on this box."""
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            fn()
+            torch.cuda.synchronize()
+        evs = [e for e in prof.events() if str(getattr(e, 'device_type', '')).endswith('CUDA')]
+        return len(evs)
+    except Exception:  # noqa: BLE001 -- a diagnostics field
+        return None
+
+
+def leg_cps_inpaint(args, dtype, K, W):
+    """A problem the fused engines do not match, on the generic per-operator device path: the
+    reference notebook's TV-LAD inpainting (CPS, K = LinOpVStack(Masking, Gradient(forward)),
+    H = ProxFuncHStack(L1Loss, mu L1Norm), G = Segment) at 2048^2 -- one kernel per operator call,
+    stopping rule on the device (proxalgs._DeviceLoop).  it/s from the difference of a (W + K)- and
+    a W-iteration iterate() (setup cancels), launches per iteration from torch.profiler's device
+    activity over the same difference."""
+    from pycsou_amd.func import L1Loss, L1Norm, ProxFuncHStack, Segment
+    from pycsou_amd.linop import Gradient, LinOpVStack, Masking
+    from pycsou_amd.opt import CPS
+    n = 2048
+    N = n * n
+    rng = np.random.default_rng(5)
+    mask = rng.random(N) < 0.5
+    img = phantom((n, n), 12, 5).ravel()
+    y = torch.from_numpy(img[mask].astype(np.float32 if dtype == torch.float32 else np.float64)).cuda()
+    Gop = Masking(size=N, sampling_bool=mask)
+    Gop.lipschitz_cst = Gop.diff_lipschitz_cst = 1.0
+    D = Gradient(shape=(n, n), kind='forward')
+    D.lipschitz_cst = D.diff_lipschitz_cst = np.sqrt(8.0)
+    Kop = LinOpVStack(Gop, D)
+    H = ProxFuncHStack(L1Loss(dim=int(mask.sum()), data=y), 0.1 * L1Norm(dim=2 * N))
+    x0 = torch.zeros(N, dtype=dtype, device='cuda')
+
+    def run(iters):
+        cps = CPS(dim=N, G=Segment(dim=N, a=0, b=1), H=H, K=Kop, x0=x0, max_iter=iters, min_iter=iters,
+                  accuracy_threshold=0.0, verbose=None)
+        cps.iterate()
+        assert cps.iter == iters + 1 or cps.iter == iters, cps.iter
+        return cps.iter
+
+    run(max(W, 2))  # warm caches / allocator
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_a = run(W)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    n_b = run(W + K)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ms = ((t2 - t1) - (t1 - t0)) * 1e3 / max(1, n_b - n_a)
+    la, lb = _kernel_launches(lambda: run(4)), _kernel_launches(lambda: run(14))
+    launches = None if la is None or lb is None else round((lb - la) / 10.0, 1)
+    elem = 4 if dtype == torch.float32 else 8
+    m = int(mask.sum())
+    alg = (1 + 1 + 1 + 2 * (m + 2 * N) / N) * N * elem  # read x, y (masked), write x'; z (m + 2N) in and out
+    return {'workload': f'CPS TV-LAD inpainting {n}x{n} {args.dtype} (reference notebook problem): K = LinOpVStack('
+                        f'Masking 50 %, Gradient(forward)), H = ProxFuncHStack(L1Loss, 0.1*L1Norm), G = Segment(0, 1); '
+                        f'generic per-operator device path (no fused match), stopping rule on the device',
+            'it_per_s': round(1e3 / ms, 1), 'ms_per_iter': round(ms, 5), 'steps': K, 'warmup': W,
+            'launches_per_iter': launches, 'alg_bytes_per_iter': int(alg),
+            'iteration_frac_of_hbm_peak': round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def slab_bench(n, dtype, K, W, world):
     """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
     (barrier + synchronize on both sides; the caller takes the max over ranks)."""
@@ -565,13 +638,13 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10',
-                    help='volume legs name:edge:dtype:steps, comma separated ("" skips them)')
+    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10,c4_cen:512:f32:20:centered',
+                    help='volume legs name:edge:dtype:steps[:kind], comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
-    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,conv63',
+    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,conv63,cps_inpaint',
                     help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
                          'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K), c3_cen (C3 with the default '
-                         'centered Gradient); "" skips them')
+                         'centered Gradient), conv63 (63x63 FFT Convolve2D), cps_inpaint (generic path); "" skips them')
     ap.add_argument('--lipschitz', default='lanczos', choices=['lanczos', 'analytic'],
                     help='operator norms of the single-GPU 2-D problems: compute_lipschitz_cst() or closed forms')
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
@@ -672,16 +745,17 @@ def main():
         if world == 1 and args.engine != 'slab':
             for leg in filter(None, args.legs.split(',')):
                 fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen,
-                      'c3_cen': leg_c3_cen, 'conv63': leg_conv63}[leg]
+                      'c3_cen': leg_c3_cen, 'conv63': leg_conv63, 'cps_inpaint': leg_cps_inpaint}[leg]
                 try:
                     out[leg] = fn(args, dtype, K, W)
                 except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
                     out[leg] = {'error': f'{type(e).__name__}: {e}'[:300]}
                     print(f'bench: leg {leg} failed: {out[leg]["error"]}', file=sys.stderr)
     for leg in filter(None, args.volumes.split(',')):
-        name, edge, vdt, vsteps = leg.split(':')
+        name, edge, vdt, vsteps, *vk = leg.split(':')
         out = volume_leg(args, out if rank == 0 else None, f'volume_{name}', int(edge),
-                         torch.float64 if vdt == 'f64' else torch.float32, int(vsteps), world, rank)
+                         torch.float64 if vdt == 'f64' else torch.float32, int(vsteps), world, rank,
+                         vk[0] if vk else 'forward')
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -689,7 +763,7 @@ def main():
         dist.destroy_process_group()
 
 
-def volume_leg(args, out, key, edge, dtype_v, steps, world, rank):
+def volume_leg(args, out, key, edge, dtype_v, steps, world, rank, kind='forward'):
     """Run volume_bench under a watchdog; `out` (rank 0) gains `key`.  A failure leaves the C3
     line as it was; a stall past --volume-timeout prints it and ends the process."""
     def fire():
@@ -704,7 +778,7 @@ def volume_leg(args, out, key, edge, dtype_v, steps, world, rank):
     timer.start()
     try:
         K = max(2, steps + steps % 2)
-        vres = volume_bench(edge, dtype_v, K, 8, world, rank)  # warmup also picks the schedule
+        vres = volume_bench(edge, dtype_v, K, 8, world, rank, kind)  # warmup also picks the schedule
     except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
         vres = {'error': f'{type(e).__name__}: {e}'[:300]}
         print(f'bench: volume leg failed: {vres["error"]}', file=sys.stderr)

@@ -407,7 +407,8 @@ int pcs_slab2d_destroy(void* plan);
  *   fkind PCS_F_NULL: 0;  PCS_F_DENOISE: x - g (g holds y);  PCS_F_GRADBUF: g.
  * Volume n0 x n1 x n2 (C order, n2 % 4 == 0); slab form as in 2-D along axis 0: the local
  * arrays hold planes [plane0 - halo, plane0 + planes + halo); `g` must supply planes
- * [0, planes] (one past the slab) when planes < n0. */
+ * [0, planes] (one past the slab) when planes < n0 -- [-1, planes] for the backward / centred
+ * kinds (kkind), which also need halo_z >= 2 (K^T z at plane p reads z0 of p - 1 .. p + 1). */
 typedef struct {
   int dtype, fkind, hkind, gkind;
   int64_t n0, n1, n2;
@@ -420,6 +421,8 @@ typedef struct {
   void* ctrl;             /* device control block; NULL = always run */
   double* hist;           /* non-NULL: in-launch reduce + loop control (single GPU) */
   void* ws;               /* with hist: pcs_pds3d_ws_bytes() bytes, zeroed once */
+  int kkind;              /* PCS_FORWARD (0), PCS_BACKWARD or PCS_CENTERED: Gradient(kind) */
+  int edge;               /* Gradient(edge=...): the centred kind's one-sided end samples */
 } pcs_pds3d_args;
 
 int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a);

@@ -62,7 +62,7 @@ class Pds3Args(ctypes.Structure):
                 ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
                 ('step0', _c_dbl), ('step1', _c_dbl), ('step2', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('g', _vp),
-                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp)]
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp), ('kkind', _c_int), ('edge', _c_int)]
 
 
 class HaloSet(ctypes.Structure):

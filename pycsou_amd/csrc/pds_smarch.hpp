@@ -33,6 +33,7 @@
 #include <type_traits>
 
 #include "pds_march.hpp"
+#include "stencil.hpp"
 
 namespace pcs {
 
@@ -53,77 +54,7 @@ enum { SK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED (2 compon
 // normal-operator kernel, pcs_conv2d_sep_ata_planes) and b = Conv^T y (formed once per problem)
 enum { SM_F_NB = 16 };
 
-// ---- the stencils on a 5-sample window w[k] = a[i + k - 2] along one axis (stencil.hpp order);
-// INT: the sample is known to lie >= 2 samples inside the axis (no edge rule applies).  hipcc
-// contracts a * b + c freely (-ffp-contract=fast ignores the fp pragmas), so every formula here is
-// written with no mul feeding an add -- (difference) * step, or an explicit fma -- and the interior
-// and the edge instantiations of a sample give the same bits: a pixel's result does not depend on
-// which row step or slab it falls in (slabs are bitwise equal to the whole image)
-__device__ __forceinline__ float sm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-
-template <int KIND, bool INT>
-__device__ __forceinline__ float sw_d1_fwd(const float (&w)[5], int i, int n, float ih, int edge) {
-  if constexpr (KIND == PCS_FORWARD) {
-    const float c = (w[3] - w[2]) * ih;
-    return (INT || i < n - 1) ? c : 0.f;
-  } else if constexpr (KIND == PCS_BACKWARD) {
-    const float c = (w[2] - w[1]) * ih;
-    return (INT || i > 0) ? c : 0.f;
-  } else {
-    const float c = (w[3] - w[1]) * (0.5f * ih);
-    if constexpr (INT) return c;
-    const float e = (i == 0) ? (w[3] - w[2]) * ih : (w[2] - w[1]) * ih;
-    return (i > 0 && i < n - 1) ? c : ((edge && n >= 2) ? e : 0.f);
-  }
-}
-// The adjoints return the stencil sum in sample units (the caller scales by 1/h): only adds and the
-// exact halving/doubling happen in here, so contraction has nothing to choose between
-template <int KIND, bool INT>
-__device__ __forceinline__ float sw_d1_adj(const float (&w)[5], int i, int n, int edge) {
-  if constexpr (KIND == PCS_FORWARD) {  // -w[2] [i < n-1] + w[1] [i > 0]
-    const float t2 = (INT || i < n - 1) ? w[2] : 0.f;
-    const float t1 = (INT || i > 0) ? w[1] : 0.f;
-    return t1 - t2;
-  } else if constexpr (KIND == PCS_BACKWARD) {
-    const float t3 = (INT || i < n - 1) ? w[3] : 0.f;
-    const float t2 = (INT || i > 0) ? w[2] : 0.f;
-    return t2 - t3;
-  } else {
-    const float t3 = (INT || i <= n - 3) ? w[3] : 0.f;
-    const float t1 = (INT || i >= 2) ? w[1] : 0.f;
-    float acc = 0.5f * (t1 - t3);
-    if (!INT && edge && n >= 2) {  // only rows within 2 of an edge, which INT never covers
-      if (i == 0) acc -= w[2];
-      if (i == 1) acc += w[1];
-      if (i == n - 2) acc -= w[3];
-      if (i == n - 1) acc += w[2];
-    }
-    return acc;
-  }
-}
-template <bool INT>
-__device__ __forceinline__ float sw_d2_fwd(const float (&w)[5], int i, int n, float ih2, int edge) {
-  const float c = ((w[3] - 2.f * w[2]) + w[1]) * ih2;  // 2 w exact: contracting the inner sub is exact
-  if constexpr (INT) return c;
-  const float e = (i == 0) ? ((w[2] - 2.f * w[3]) + w[4]) * ih2 : ((w[0] - 2.f * w[1]) + w[2]) * ih2;
-  return (i > 0 && i < n - 1) ? c : ((edge && n >= 3) ? e : 0.f);
-}
-template <bool INT>
-__device__ __forceinline__ float sw_d2_adj(const float (&w)[5], int i, int n, int edge) {
-  const float t3 = (INT || i <= n - 3) ? w[3] : 0.f;
-  const float t2 = (INT || (i >= 1 && i <= n - 2)) ? w[2] : 0.f;
-  const float t1 = (INT || i >= 2) ? w[1] : 0.f;
-  float acc = (t3 - 2.f * t2) + t1;
-  if (!INT && edge && n >= 3) {
-    if (i == 0) acc += w[2];
-    if (i == 1) acc -= 2.f * w[1];
-    if (i == 2) acc += w[0];
-    if (i == n - 3) acc += w[4];
-    if (i == n - 2) acc -= 2.f * w[3];
-    if (i == n - 1) acc += w[2];
-  }
-  return acc;
-}
+// the stencils on a 5-sample window: stencil.hpp (sw_d1_fwd / sw_d1_adj / sw_d2_fwd / sw_d2_adj)
 
 // stencil-specific parameters (the rest is Params<float>)
 struct SParams {
@@ -293,9 +224,9 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
       }
       T kt;
       if constexpr (KK == SK_LAP) {
-        kt = sm_fma(Q.w0 * Q.ih20, sw_d2_adj<RI>(w0, gr_, n0, edge), (Q.w1 * Q.ih21) * sw_d2_adj<CI>(w1, i1, n1, edge));
+        kt = pcs_fma(Q.w0 * Q.ih20, sw_d2_adj<RI>(w0, gr_, n0, edge), (Q.w1 * Q.ih21) * sw_d2_adj<CI>(w1, i1, n1, edge));
       } else {  // VStack rmatvec: D0^T z0 + D1^T z1
-        kt = sm_fma(sw_d1_adj<KK, RI>(w0, gr_, n0, edge), P.inv_step0,
+        kt = pcs_fma(sw_d1_adj<KK, RI>(w0, gr_, n0, edge), P.inv_step0,
                     sw_d1_adj<KK, CI>(w1, i1, n1, edge) * P.inv_step1);
       }
       const T xv = m < 4 ? xr[PB].v[m] : xe[PB];
@@ -308,7 +239,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
       const T u = in ? (T(2) * xt - xv) : T(0);
       if (m < 4) {
         uo.v[m] = u;
-        const T xnew = sm_fma(P.rho, xt, P.omr * xv);
+        const T xnew = pcs_fma(P.rho, xt, P.omr * xv);
         xo.v[m] = xnew;
         const T dx = xv - xnew;
         sdx += dx * dx;
@@ -359,7 +290,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
       }
       T ku[D];
       if constexpr (KK == SK_LAP) {  // w0 D2_0 u + w1 D2_1 u (pylops Laplacian matvec)
-        ku[0] = sm_fma(Q.w0, sw_d2_fwd<RI>(w0, gr_, n0, Q.ih20, edge), Q.w1 * sw_d2_fwd<CI>(w1, i1, n1, Q.ih21, edge));
+        ku[0] = pcs_fma(Q.w0, sw_d2_fwd<RI>(w0, gr_, n0, Q.ih20, edge), Q.w1 * sw_d2_fwd<CI>(w1, i1, n1, Q.ih21, edge));
       } else {
         ku[0] = sw_d1_fwd<KK, RI>(w0, gr_, n0, P.inv_step0, edge);
         ku[D - 1] = sw_d1_fwd<KK, CI>(w1, i1, n1, P.inv_step1, edge);
@@ -371,7 +302,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
         v[d] = w[d] * P.inv_sigma;
       }
       if constexpr (D == 2 && HK == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
-        T f = T(1) - P.t_h * fast_rsqrt(sm_fma(v[0], v[0], v[D - 1] * v[D - 1]));
+        T f = T(1) - P.t_h * fast_rsqrt(pcs_fma(v[0], v[0], v[D - 1] * v[D - 1]));
         f = f > T(0) ? f : T(0);
 #pragma unroll
         for (int d = 0; d < D; ++d) zt[d] = w[d] - P.sigma * (f * v[d]);
@@ -381,7 +312,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
       }
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        o[d].v[m] = sm_fma(P.rho, zt[d], P.omr * zv[d].v[m]);
+        o[d].v[m] = pcs_fma(P.rho, zt[d], P.omr * zv[d].v[m]);
         const T ed = zv[d].v[m] - o[d].v[m];
         sdz += ed * ed;
         sz += zv[d].v[m] * zv[d].v[m];

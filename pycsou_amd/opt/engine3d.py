@@ -3,7 +3,7 @@
 Problem family (what a reference script builds for 3-D TV deconvolution / denoising):
 ``F = (1/2) * SquaredL2Loss(dim, data=y) [* C]`` with ``C`` a composition of
 ``Convolve1D(size, taps, reshape_dims=shape, axis=k)`` (the reference's only 3-D blur,
-``pycsou/linop/conv.py:20-164``), ``K = Gradient(shape, kind='forward')`` in 3-D
+``pycsou/linop/conv.py:20-164``), ``K = Gradient(shape, kind=...)`` in 3-D (forward; backward / centred through k_pds3d_gen)
 (``pycsou/linop/diff.py:777-882``), ``H = lam * L21Norm(groups=tile(arange(N), 3))`` or
 ``lam * L1Norm``, ``G = None / NonNegativeOrthant / Segment``.
 
@@ -55,11 +55,15 @@ def conv_chain(C, shape):
 
 def match_pds3d(F, G, H, K, has_H):
     """Engine spec dict if (F, G, H, K) is a fused 3-D problem, else None."""
-    if not has_H or not isinstance(K, GradientOp) or len(K.dims) != 3 or K.kind != 'forward':
+    if not has_H or not isinstance(K, GradientOp) or len(K.dims) != 3:
+        return None
+    kinds = {'forward': L.PCS_FORWARD, 'backward': L.PCS_BACKWARD, 'centered': L.PCS_CENTERED}
+    if K.kind not in kinds:
         return None
     shape = tuple(K.dims)
     N = int(np.prod(shape))
-    spec = {'ndim': 3, 'shape': shape, 'steps': tuple(K.steps)}
+    # kkind: forward -> k_pds3d; backward / centred (the reference's default) -> k_pds3d_gen
+    spec = {'ndim': 3, 'shape': shape, 'steps': tuple(K.steps), 'kkind': kinds[K.kind], 'edge': int(K.edge)}
     base, lam = H, 1.0
     if isinstance(H, ProxFuncPostComp):
         if H.shift != 0:
@@ -132,11 +136,15 @@ class PDS3DEngine:
                 if op.axis == 0:
                     reach += max(off, k - 1 - off)
         hx = 2 * reach + 1 if fk == L.PCS_F_GRADBUF else 1
-        hz = 1
+        self.kkind = spec.get('kkind', L.PCS_FORWARD)
+        # backward / centred K: K^T z at plane p reads z0(p + 1) and u is needed one plane below
+        # the slab too (K u reaches back): z halo 2, and g on planes [-1, rows] (g_lo below)
+        hz = 1 if self.kkind == L.PCS_FORWARD else 2
         hg = hx if fk == L.PCS_F_GRADBUF else 1
         if world > 1 and self.rows < max(hx, hz):
             raise ValueError(f'slab of {self.rows} planes is thinner than its halo ({hx} planes)')
         self.hx, self.hz, self.hg = hx, hz, hg
+        self.g_lo = hx if self.kkind == L.PCS_FORWARD else hx - 1  # first sub-volume plane of g the update reads
         N = n0 * plane
         x0d, z0d = O.to_dev(x0, dtype), O.to_dev(z0, dtype)
         self.X = [lay.window(x0d, hx) for _ in range(2)]
@@ -218,6 +226,7 @@ class PDS3DEngine:
         a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
         a.step0, a.step1, a.step2 = spec['steps']
         a.seg_a, a.seg_b = spec['seg']
+        a.kkind, a.edge = self.kkind, spec.get('edge', 0)
         if fk == L.PCS_F_DENOISE:
             a.g = self.yw.data_ptr()
         elif fk == L.PCS_F_GRADBUF:
@@ -286,7 +295,7 @@ class PDS3DEngine:
         plane = self.plane
         if self.ata:
             self._ata_planes(L.ptr(self.X[p]), L.ptr(self.T[0]), nsub, st)
-            self._g_range(self.hx, min(self.hx + self.rows + 1, nsub), st)
+            self._g_range(self.g_lo, min(self.hx + self.rows + 1, nsub), st)
             return
         cur, j = self.X[p], 0
         if self.sep2:
@@ -299,7 +308,8 @@ class PDS3DEngine:
                 self._conv_into(cur, dst, axis, h, k, off, st)
                 cur, j = dst, j + 1
         # s on the planes the update reads: own planes + the next one (u on the slab's last plane + 1)
-        q0, q1 = self.hx, min(self.hx + self.rows + 1, nsub)
+        # and, for backward / centred K, the one before
+        q0, q1 = self.g_lo, min(self.hx + self.rows + 1, nsub)
         img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0
         _, h, _, k, off = self.ax0
         dst = self.T[j % 2]
@@ -361,11 +371,12 @@ class PDS3DEngine:
         nsub = R + 2 * hx
         self._sep_range(self.X[p], self.T[0], 0, hx, False, st)
         self._sep_range(self.X[p], self.T[0], hx + R, nsub, False, st)
+        g0 = self.g_lo  # hx, or hx - 1 for backward / centred K (u one plane before each band)
         if self.order == 'fullg':  # g on every plane the update reads, one axis-0 launch
-            self._g_range(hx, min(hx + R + 1, nsub), st)
+            self._g_range(g0, min(hx + R + 1, nsub), st)
         else:
-            self._g_range(hx, hx + B + 1, st)
-            self._g_range(hx + R - B, min(hx + R + 1, nsub), st)
+            self._g_range(g0, hx + B + 1, st)
+            self._g_range(hx + R - B - (hx - g0), min(hx + R + 1, nsub), st)
         a = self.args[p]
         a.hist = None
         a.partials = self.partials.data_ptr()

@@ -93,6 +93,7 @@ def main():
 
     PyLop = R.lbase.PyLopLinearOperator
     out = {}
+    only = [c for c in os.environ.get('GOLDEN_ONLY', '').split(',') if c]  # regenerate just these PDS cases
 
     # ---------------- prox / functional known answers ----------------
     pen, loss = R.penalty, R.loss
@@ -129,7 +130,8 @@ def main():
         'doc_sql2_arange': np.array(pen.SquaredL2Norm(10)(x10)),
         'doc_soft': R.mprox.soft(np.linspace(-1, 1, 5), 0.5),
     }
-    np.savez(os.path.join(HERE, 'prox.npz'), **f)
+    if not only:
+        np.savez(os.path.join(HERE, 'prox.npz'), **f)
     print('prox.npz', {k: np.shape(a) for k, a in f.items()})
 
     # ---------------- operator goldens (PyLops boundary) ----------------
@@ -151,7 +153,8 @@ def main():
     xd = np.repeat([0, 2, 1, 3, 0, 2, 0], 10).astype(np.float64)
     ops['doc_d1_x'] = xd
     ops['doc_d1_y'] = np.diff(xd, append=0)  # diff.py:72-78
-    np.savez(os.path.join(HERE, 'ops.npz'), **ops)
+    if not only:
+        np.savez(os.path.join(HERE, 'ops.npz'), **ops)
 
     # ---------------- solver trajectories from the reference PDS / APGD ----------------
     PDS, APGD = R.proxalgs.PDS, R.proxalgs.APGD
@@ -223,11 +226,19 @@ def main():
         'deconv3d_l21_fwd_24_sep15': dict(shape=(24, 20, 22), psf=None, conv1d=gaussian_taps(15, 2.0), lam=0.05,
                                           kind='forward', hname='l21', niter=20),
         'denoise3d_l1_fwd_16': dict(shape=(16, 17, 18), psf=None, lam=0.1, kind='forward', hname='l1', niter=15),
+        # 3-D with the reference's default centred Gradient and the backward kind (k_pds3d_gen)
+        'denoise3d_l21_cen_16': dict(shape=(16, 17, 20), psf=None, lam=0.1, kind='centered', hname='l21', niter=15),
+        'deconv3d_l1_bwd_20_sep7': dict(shape=(20, 18, 24), psf=None, conv1d=gaussian_taps(7, 1.2), lam=0.05,
+                                        kind='backward', hname='l1', niter=15),
+        'deconv3d_l21_cen_24_sep15': dict(shape=(24, 20, 24), psf=None, conv1d=gaussian_taps(15, 2.0), lam=0.05,
+                                          kind='centered', hname='l21', niter=15),
         # natural termination (accuracy_threshold=1e-3, min_iter=10): pins the iteration-count semantics
         'denoise2d_l21_fwd_32_stop': dict(shape=(32, 32), psf=None, lam=0.1, kind='forward', hname='l21',
                                           niter=500, thr=1e-3, min_iter=10),
     }
     for name, kw in cases.items():
+        if only and name not in only:
+            continue
         res = run_pds(**kw)
         meta = dict(kw)
         psf = meta.pop('psf')
@@ -243,6 +254,8 @@ def main():
         np.savez_compressed(os.path.join(HERE, f'pds_{name}.npz'), **arrays)
         print(name, 'iters', res['n_iter'], 'last rel', res['diag_primal'][-1])
 
+    if only:
+        return
     # ---------------- APGD LASSO (C1), CD and BT ----------------
     rng = np.random.default_rng(0)
     A = rng.standard_normal((256, 512))

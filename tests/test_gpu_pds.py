@@ -253,7 +253,7 @@ def test_pds3d_ata_opt_in_matches_reference(monkeypatch, dtype):
     assert rel(est['dual_variable'], z_ref) < tol
 
 
-def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None):
+def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None, kind='forward'):
     """A 3-D TV deconvolution case (separable 15-tap Gaussian along every axis), built like
     the golden cases so tests/cases.oracle_pds can run it."""
     rng = np.random.default_rng(seed)
@@ -273,7 +273,7 @@ def _vol_problem(n, dtype, seed=0, lam=0.05, niter=10, shape=None):
         v = P.Convolve1D(N, taps, offset=7, dims=shape, dir=a).matvec(v)
     y = v + 0.01 * rng.standard_normal(N)
     c = {'shape': shape, 'taps': taps, 'y': y,
-         'meta': {'kind': 'forward', 'hname': 'l21', 'lam': lam, 'niter': niter}}
+         'meta': {'kind': kind, 'hname': 'l21', 'lam': lam, 'niter': niter}}
     return c
 
 
@@ -400,3 +400,24 @@ def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
     tol = 1e-10 if dtype == np.float64 else 5e-5
     assert rel(est['primal_variable'], x_ref) < tol
     assert rel(est['dual_variable'], z_ref) < tol
+
+
+@pytest.mark.parametrize('shape,dtype,kind', [((20, 36, 260), np.float64, 'centered'), ((17, 9, 132), np.float32, 'centered'),
+                                              ((12, 33, 130), np.float64, 'backward'), ((24, 20, 24), np.float32, 'backward')])
+def test_pds3d_general_k_vs_oracle(shape, dtype, kind):
+    """Backward / centred 3-D Gradient (the reference's default kind) through the general-K plane
+    march (k_pds3d_gen): ragged tiles (last column tile of 4 or 2 columns, rows not a multiple of
+    8), 15-tap blur along every axis, against the CPU oracle (8 iterations)."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    c = _vol_problem(0, dtype, seed=5, niter=8, shape=shape, kind=kind)
+    pds = build(c, dtype, engine='fused')
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    est, _, diag = pds.iterate()
+    assert isinstance(pds._engine, PDS3DEngine) and pds._engine.kkind != 0
+    assert pds.iter == 8
+    x_ref, z_ref, d_ref = oracle_pds(c)
+    tol = 1e-10 if dtype == np.float64 else 5e-5
+    assert rel(est['primal_variable'], x_ref) < tol
+    assert rel(est['dual_variable'], z_ref) < tol
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:],
+                               np.asarray(d_ref['primal'])[1:], rtol=1e-8 if dtype == np.float64 else 1e-3)

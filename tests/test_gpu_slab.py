@@ -354,15 +354,51 @@ def test_native_loop_early_stop(overlap):
     assert np.allclose(h2[1:2 * n], h1[1:2 * n], rtol=1e-5)
 
 
-def vol3d_case(n0=80, seed=3, niter=8):
+def vol3d_case(n0=80, seed=3, niter=8, kind='forward'):
     """n0 x 24 x 20 TV deconvolution (15-tap blur along every axis): slabs of >= 33 planes
     take the banded 3-D schedule (boundary bands of hx + 1 = 16 planes)."""
     from tests.test_gpu_pds import _vol_problem
-    c = _vol_problem(24, np.float64, seed=seed, niter=niter)
+    c = _vol_problem(24, np.float64, seed=seed, niter=niter, kind=kind)
     rng = np.random.default_rng(seed + 1)
     c['shape'] = (n0, 24, 20)
     c['y'] = rng.uniform(0, 1, n0 * 24 * 20)
     return c
+
+
+@pytest.mark.parametrize('name,world', [('denoise3d_l21_cen_16', 2), ('denoise3d_l21_cen_16', 3),
+                                        ('deconv3d_l1_bwd_20_sep7', 2)])
+def test_slab3d_general_k_bitwise(name, world):
+    """Backward / centred 3-D K (k_pds3d_gen: z halo 2, g on planes [-1, rows]) on 2-3 plane
+    slabs in one process: x, z bitwise equal to the single-GPU engine, iteration count of the
+    reference golden."""
+    for dtype in (np.float64, np.float32):
+        c = pds_case(name)
+        pds = build(c, dtype, engine='fused')
+        (n1, x1, z1, h1), (n2, x2, z2, h2) = _pds3d_single_and_slabs(pds, world)
+        assert n1 == int(c['n_iter'])
+        assert torch.equal(x2, x1), (dtype, (x2 - x1).abs().max().item())
+        assert torch.equal(z2, z1), (dtype, (z2 - z1).abs().max().item())
+
+
+@pytest.mark.parametrize('kind', ['centered', 'backward'])
+def test_slab3d_banded_general_k_bitwise(kind):
+    """The banded 3-D order with a backward / centred K (g of the plane before each band too):
+    3 slabs of 100 planes, fp32, bitwise the single-GPU engine."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    from pycsou_amd.parallel import run_local
+    pds = build(vol3d_case(100, kind=kind), np.float32, engine='fused')
+    spec = pds._fused_spec()
+    dt = pds._compute_dtype()
+    one = PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    n1, x1, z1, h1 = one.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
+    slabs = [PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank=r, world=3) for r in range(3)]
+    assert all(s.banded and s.hz == 2 for s in slabs)
+    res = run_local(slabs, pds.max_iter, pds.min_iter, pds.accuracy_threshold, split=True)
+    assert all(r[0] == n1 == 8 for r in res)
+    x2 = torch.cat([r[1] for r in res])
+    z2 = torch.cat([torch.cat([r[2].view(3, -1)[c] for r in res]) for c in range(3)])
+    assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
+    assert torch.equal(z2, z1)
 
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
