@@ -17,6 +17,8 @@
 // p's work.  Every load goes through a buffer descriptor of ONE plane (num_records = 0 for a
 // plane outside the image or the stored slab, so those read 0) with in-plane rows / columns
 // outside the image pushed past the range: no branches, no selects.
+#include <type_traits>
+
 #include "pds_march.hpp"
 #include "stencil.hpp"
 
@@ -354,7 +356,11 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
 // same arithmetic for every voxel (no interior specialisation), so slabs are bitwise the whole
 // volume.  Traffic per voxel: x, g, z (3) in; x', z' (3) out = 9 words (the forward kernel's),
 // plus the tile halos (rows +- 1, one 4-group per side).
-constexpr int k3gT1 = 8, k3gTW = 128, k3gNT = 512;
+// Tile rows: 16 for fp32 (vertical halo 2/16: PMC reads 1.39x -> ~1.24x the algorithmic at 8 rows;
+// 101 KB of LDS), 8 for fp64 (the 16-row rings would need 202 KB)
+constexpr int k3gTW = 128, k3gNT = 512;
+template <typename T>
+constexpr int k3g_rows() { return sizeof(T) == 4 ? 16 : 8; }
 
 template <typename T, int KK, int FK, bool VEC>
 __global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T*
                                                      const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk, int edge,
                                                      double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
                                                      int tiles1, int tiles2, Bands bd, int ntasks) {
-  constexpr int T1 = k3gT1, TW = k3gTW, NT = k3gNT;
+  constexpr int T1 = k3g_rows<T>(), TW = k3gTW, NT = k3gNT;
   constexpr int UR = T1 + 2, UG = TW / 4 + 2, WU = 4 * UG;  // u / z0 region: rows r1-1 .. r1+T1, cols c2-4 ..
   constexpr int R1 = T1 + 4, W2G = UG + 2, W2 = 4 * W2G;    // z1 rows r1-2 .. r1+T1+1; z2 cols c2-8 .. c2+TW+8
   constexpr int NU = UR * UG, NZ1 = R1 * UG, NZ2 = UR * W2G, NZ = T1 * (TW / 4);
@@ -414,33 +420,42 @@ __global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T*
   }
   const int ze = min(tid, NZ - 1), zi = ze / (TW / 4), zg = ze - zi * (TW / 4);
   const int i1z = r1 + zi, c_z = c2 + 4 * zg;
+  // the tile's u region (rows r1-1 .. r1+T1, cols c2-4 .. c2+TW+3) >= 2 samples inside the plane
+  const bool tile_int = r1 - 1 >= 2 && r1 + T1 <= v.n1 - 3 && c2 - 4 >= 2 && c2 + TW + 3 <= v.n2 - 3;
 
-  G4<T> xr[KU], gr[KU], z0r[KU], z1r[K1], z2r[K2];
-  auto prefetch = [&](int p) {  // x, g, z1, z2 of plane p; z0 of plane p + 1
+  // loads run two planes ahead: iteration p lands set p & 1 and refills it with plane p + 2's data
+  // (C4 centred: 1.41 ms with one set; the wait for the next plane's loads was exposed at two waves
+  // per SIMD)
+  G4<T> xr[2][KU], gr[2][KU], z0r[2][KU], z1r[2][K1], z2r[2][K2];
+  auto prefetch = [&](int p, auto sc) {  // x, g, z1, z2 of plane p; z0 of plane p + 1 -> set sc
+    constexpr int S = decltype(sc)::value;
     const Rsrc rx = plane_rsrc(x, v, v.hx, p), rz0 = plane_rsrc(z, v, v.hz, p + 1),
                rz1 = plane_rsrc(z + zstride, v, v.hz, p), rz2 = plane_rsrc(z + 2 * zstride, v, v.hz, p);
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
-      xr[k] = gload<T, VEC>(rx, off_u[k]);
-      if constexpr (FK != PCS_F_NULL) gr[k] = gload<T, VEC>(plane_rsrc(g, v, v.hg, p), off_u[k]);
-      z0r[k] = gload<T, VEC>(rz0, off_u[k]);
+      xr[S][k] = gload<T, VEC>(rx, off_u[k]);
+      if constexpr (FK != PCS_F_NULL) gr[S][k] = gload<T, VEC>(plane_rsrc(g, v, v.hg, p), off_u[k]);
+      z0r[S][k] = gload<T, VEC>(rz0, off_u[k]);
     }
 #pragma unroll
-    for (int k = 0; k < K1; ++k) z1r[k] = gload<T, VEC>(rz1, off_1[k]);
+    for (int k = 0; k < K1; ++k) z1r[S][k] = gload<T, VEC>(rz1, off_1[k]);
 #pragma unroll
-    for (int k = 0; k < K2; ++k) z2r[k] = gload<T, VEC>(rz2, off_2[k]);
+    for (int k = 0; k < K2; ++k) z2r[S][k] = gload<T, VEC>(rz2, off_2[k]);
   };
-  auto land = [&](int s3, int s2) {  // z0 slot s3 (plane p + 1), z1 / z2 slot s2 (plane p)
+  auto land = [&](int s3, int s2, auto sc) {  // z0 slot s3 (plane p + 1), z1 / z2 slot s2 (plane p)
+    constexpr int S = decltype(sc)::value;
 #pragma unroll
     for (int k = 0; k < KU; ++k)
-      if (k * NT + tid < NU) st4(&Z0[s3][ui[k] * WU + 4 * ug[k]], z0r[k]);
+      if (k * NT + tid < NU) st4(&Z0[s3][ui[k] * WU + 4 * ug[k]], z0r[S][k]);
 #pragma unroll
     for (int k = 0; k < K1; ++k)
-      if (k * NT + tid < NZ1) st4(&Z1[s2][(k * NT + tid) * 4], z1r[k]);  // row-major, pitch WU
+      if (k * NT + tid < NZ1) st4(&Z1[s2][(k * NT + tid) * 4], z1r[S][k]);  // row-major, pitch WU
 #pragma unroll
     for (int k = 0; k < K2; ++k)
-      if (k * NT + tid < NZ2) st4(&Z2[s2][(k * NT + tid) * 4], z2r[k]);  // row-major, pitch W2
+      if (k * NT + tid < NZ2) st4(&Z2[s2][(k * NT + tid) * 4], z2r[S][k]);  // row-major, pitch W2
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   // ring slots: plane j lives in slot (j + 3 * 2^20) % 3 of the 3-plane rings, (j & 1) of the others
@@ -457,124 +472,141 @@ __global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T*
       }
     }
   }
-  prefetch(p_start - 1);
-  for (int p = p_start - 1; p <= p_end; ++p) {
+  prefetch(p_start - 1, S0{});
+  if (p_start <= p_end) prefetch(p_start, S1{});
+  auto iter = [&](int p, auto sc) {
+    constexpr int S = decltype(sc)::value;
     const int sm1 = slot3(p - 1), s0 = slot3(p), sp1 = slot3(p + 1), sm2 = slot3(p - 2);
-    const int b2 = p & 1;
-    const int gp = v.plane0 + p;
-    lds_barrier();  // iteration p-1's z' items are done with the slots landed / written below
-    G4<T> xv4[KU], gv4[KU];
+      const int b2 = p & 1;
+      const int gp = v.plane0 + p;
+      lds_barrier();  // iteration p-1's z' items are done with the slots landed / written below
+      G4<T> xv4[KU], gv4[KU];
 #pragma unroll
-    for (int k = 0; k < KU; ++k) {
-      xv4[k] = xr[k];
-      if constexpr (FK != PCS_F_NULL) gv4[k] = gr[k];
-    }
-    land(sp1, b2);
-    if (p < p_end) prefetch(p + 1);
-    lds_barrier();
-    // ---- U items: x_t, u on the u region of plane p; x' on own voxels
-#pragma unroll
-    for (int k = 0; k < KU; ++k) {
-      if (k * NT + tid >= NU) continue;
-      const int i1 = r1 - 1 + ui[k], c = c2 - 4 + 4 * ug[k];
-      const int o = ui[k] * WU + 4 * ug[k];
-      const G4<T> za = lds4(&Z0[sm1][o]), zb = lds4(&Z0[s0][o]), zc = lds4(&Z0[sp1][o]);
-      const int o1 = (ui[k] + 1) * WU + 4 * ug[k];  // z1 region row of i1
-      const G4<T> y0 = lds4(&Z1[b2][o1 - WU]), y1 = lds4(&Z1[b2][o1]), y2 = lds4(&Z1[b2][o1 + WU]);
-      const int o2 = ui[k] * W2 + 4 * (ug[k] + 1);  // z2 region group of c
-      const G4<T> wl = lds4(&Z2[b2][o2 - 4]), wc = lds4(&Z2[b2][o2]), wr = lds4(&Z2[b2][o2 + 4]);
-      const T h2[6] = {wl.v[3], wc.v[0], wc.v[1], wc.v[2], wc.v[3], wr.v[0]};
-      const bool rin = (unsigned)i1 < (unsigned)v.n1, pin = gp >= 0 && gp < v.n0;
-      const bool own = rin && pin && ui[k] >= 1 && ui[k] <= T1 && ug[k] >= 1 && ug[k] <= TW / 4 && c < v.n2 &&
-                       p >= p_start && p < p_end;
-      G4<T> uo, xo;
-      T sdx = T(0), sx = T(0);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int i2 = c + m;
-        const bool in = rin && pin && (unsigned)i2 < (unsigned)v.n2;
-        const T w0[5] = {T(0), za.v[m], zb.v[m], zc.v[m], T(0)};
-        const T w1[5] = {T(0), y0.v[m], y1.v[m], y2.v[m], T(0)};
-        const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
-        // K^T z, VStack order ((D0^T z0 + D1^T z1) + D2^T z2), each sum scaled by 1/h once
-        const T kt = pcs_fma(sw_d1_adj<KK, false>(w2, i2, v.n2, edge), P.inv_step[2],
-                             pcs_fma(sw_d1_adj<KK, false>(w1, i1, v.n1, edge), P.inv_step[1],
-                                     sw_d1_adj<KK, false>(w0, gp, v.n0, edge) * P.inv_step[0]));
-        const T xv = xv4[k].v[m];
-        T gf;
-        if constexpr (FK == PCS_F_NULL) gf = T(0);
-        else if constexpr (FK == PCS_F_DENOISE) gf = xv - gv4[k].v[m];
-        else gf = gv4[k].v[m];
-        const T xt = prox_g((xv - P.tau * gf) - P.tau * kt, gk, P.seg_a, P.seg_b);
-        uo.v[m] = in ? (T(2) * xt - xv) : T(0);
-        const T xnew = pcs_fma(P.rho, xt, P.omr * xv);
-        xo.v[m] = xnew;
-        const T dx = xv - xnew;
-        sdx += in ? dx * dx : T(0);
-        sx += in ? xv * xv : T(0);
+      for (int k = 0; k < KU; ++k) {
+        xv4[k] = xr[S][k];
+        if constexpr (FK != PCS_F_NULL) gv4[k] = gr[S][k];
       }
-      if (own) {
-        part[0] += (double)sdx;
-        part[1] += (double)sx;
-        gstore<T, VEC>(xn + (int64_t)(p + v.hx) * pl + (int64_t)i1 * v.n2 + c, xo, c, v.n2);
-      }
-      st4(&U[s0][o], uo);
-    }
-    lds_barrier();
-    // ---- z' items for plane q = p - 1 (own tile)
-    if (p > p_start && tid < NZ) {
-      const int q = p - 1, gq = gp - 1;
-      const int o = (zi + 1) * WU + 4 * (zg + 1);
-      const G4<T> ua = lds4(&U[sm2][o]), ub = lds4(&U[sm1][o]), uc = lds4(&U[s0][o]);  // u(q-1), u(q), u(q+1)
-      const G4<T> un = lds4(&U[sm1][o - WU]), us = lds4(&U[sm1][o + WU]);             // rows i1-1, i1+1
-      const G4<T> ul = lds4(&U[sm1][o - 4]), ur = lds4(&U[sm1][o + 4]);               // groups left / right
-      const T h2[6] = {ul.v[3], ub.v[0], ub.v[1], ub.v[2], ub.v[3], ur.v[0]};
-      const G4<T> zv0 = lds4(&Z0[sm1][o]);
-      const G4<T> zv1 = lds4(&Z1[b2 ^ 1][(zi + 2) * WU + 4 * (zg + 1)]);
-      const G4<T> zv2 = lds4(&Z2[b2 ^ 1][(zi + 1) * W2 + 4 * (zg + 2)]);
-      const bool own = i1z < v.n1 && gq >= 0 && gq < v.n0 && c_z < v.n2;
-      G4<T> o0, o1, o2;
-      T sdz = T(0), sz = T(0);
+      land(sp1, b2, sc);
+      if (p + 2 <= p_end) prefetch(p + 2, sc);
+      lds_barrier();
+      // ---- U items: x_t, u on the u region of plane p; x' on own voxels (I: every sample of the
+      // tile's u region and plane p lies >= 2 samples inside the volume -- no edge rules)
+      auto u_items = [&](auto intc) {
+        constexpr bool I = decltype(intc)::value;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int i2 = c_z + m;
-        const bool cm = VEC ? true : (i2 < v.n2);
-        const T w0[5] = {T(0), ua.v[m], ub.v[m], uc.v[m], T(0)};
-        const T w1[5] = {T(0), un.v[m], ub.v[m], us.v[m], T(0)};
-        const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
-        const T k0 = sw_d1_fwd<KK, false>(w0, gq, v.n0, P.inv_step[0], edge);
-        const T k1 = sw_d1_fwd<KK, false>(w1, i1z, v.n1, P.inv_step[1], edge);
-        const T k2 = sw_d1_fwd<KK, false>(w2, i2, v.n2, P.inv_step[2], edge);
-        const T w0v = zv0.v[m] + P.sigma * k0, w1v = zv1.v[m] + P.sigma * k1, w2v = zv2.v[m] + P.sigma * k2;
-        const T v0 = w0v * P.inv_sigma, v1 = w1v * P.inv_sigma, v2 = w2v * P.inv_sigma;
-        T t0, t1, t2;
-        if (hk == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
-          T f = T(1) - P.t_h * fast_rsqrt(pcs_fma(v0, v0, pcs_fma(v1, v1, v2 * v2)));
-          f = f > T(0) ? f : T(0);
-          t0 = w0v - P.sigma * (f * v0);
-          t1 = w1v - P.sigma * (f * v1);
-          t2 = w2v - P.sigma * (f * v2);
-        } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
-          t0 = w0v - P.sigma * (v0 - P.t_h * clip1(v0 * P.inv_t_h));
-          t1 = w1v - P.sigma * (v1 - P.t_h * clip1(v1 * P.inv_t_h));
-          t2 = w2v - P.sigma * (v2 - P.t_h * clip1(v2 * P.inv_t_h));
+        for (int k = 0; k < KU; ++k) {
+          if (k * NT + tid >= NU) continue;
+          const int i1 = r1 - 1 + ui[k], c = c2 - 4 + 4 * ug[k];
+          const int o = ui[k] * WU + 4 * ug[k];
+          const G4<T> za = lds4(&Z0[sm1][o]), zb = lds4(&Z0[s0][o]), zc = lds4(&Z0[sp1][o]);
+          const int o1 = (ui[k] + 1) * WU + 4 * ug[k];  // z1 region row of i1
+          const G4<T> y0 = lds4(&Z1[b2][o1 - WU]), y1 = lds4(&Z1[b2][o1]), y2 = lds4(&Z1[b2][o1 + WU]);
+          const int o2 = ui[k] * W2 + 4 * (ug[k] + 1);  // z2 region group of c
+          const G4<T> wl = lds4(&Z2[b2][o2 - 4]), wc = lds4(&Z2[b2][o2]), wr = lds4(&Z2[b2][o2 + 4]);
+          const T h2[6] = {wl.v[3], wc.v[0], wc.v[1], wc.v[2], wc.v[3], wr.v[0]};
+          const bool rin = (unsigned)i1 < (unsigned)v.n1, pin = gp >= 0 && gp < v.n0;
+          const bool own = rin && pin && ui[k] >= 1 && ui[k] <= T1 && ug[k] >= 1 && ug[k] <= TW / 4 && c < v.n2 &&
+                           p >= p_start && p < p_end;
+          G4<T> uo, xo;
+          T sdx = T(0), sx = T(0);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int i2 = c + m;
+            const bool in = rin && pin && (unsigned)i2 < (unsigned)v.n2;
+            const T w0[5] = {T(0), za.v[m], zb.v[m], zc.v[m], T(0)};
+            const T w1[5] = {T(0), y0.v[m], y1.v[m], y2.v[m], T(0)};
+            const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
+            // K^T z, VStack order ((D0^T z0 + D1^T z1) + D2^T z2), each sum scaled by 1/h once
+            const T kt = pcs_fma(sw_d1_adj<KK, I>(w2, i2, v.n2, edge), P.inv_step[2],
+                                 pcs_fma(sw_d1_adj<KK, I>(w1, i1, v.n1, edge), P.inv_step[1],
+                                         sw_d1_adj<KK, I>(w0, gp, v.n0, edge) * P.inv_step[0]));
+            const T xv = xv4[k].v[m];
+            T gf;
+            if constexpr (FK == PCS_F_NULL) gf = T(0);
+            else if constexpr (FK == PCS_F_DENOISE) gf = xv - gv4[k].v[m];
+            else gf = gv4[k].v[m];
+            const T xt = prox_g((xv - P.tau * gf) - P.tau * kt, gk, P.seg_a, P.seg_b);
+            uo.v[m] = in ? (T(2) * xt - xv) : T(0);
+            const T xnew = pcs_fma(P.rho, xt, P.omr * xv);
+            xo.v[m] = xnew;
+            const T dx = xv - xnew;
+            sdx += in ? dx * dx : T(0);
+            sx += in ? xv * xv : T(0);
+          }
+          if (own) {
+            part[0] += (double)sdx;
+            part[1] += (double)sx;
+            gstore<T, VEC>(xn + (int64_t)(p + v.hx) * pl + (int64_t)i1 * v.n2 + c, xo, c, v.n2);
+          }
+          st4(&U[s0][o], uo);
         }
-        o0.v[m] = pcs_fma(P.rho, t0, P.omr * zv0.v[m]);
-        o1.v[m] = pcs_fma(P.rho, t1, P.omr * zv1.v[m]);
-        o2.v[m] = pcs_fma(P.rho, t2, P.omr * zv2.v[m]);
-        const T e0 = zv0.v[m] - o0.v[m], e1 = zv1.v[m] - o1.v[m], e2 = zv2.v[m] - o2.v[m];
-        sdz += cm ? pcs_fma(e0, e0, pcs_fma(e1, e1, e2 * e2)) : T(0);
-        sz += cm ? pcs_fma(zv0.v[m], zv0.v[m], pcs_fma(zv1.v[m], zv1.v[m], zv2.v[m] * zv2.v[m])) : T(0);
-      }
-      if (own) {
-        part[2] += (double)sdz;
-        part[3] += (double)sz;
-        T* d = zn + (int64_t)(q + v.hz) * pl + (int64_t)i1z * v.n2 + c_z;
-        gstore<T, VEC>(d, o0, c_z, v.n2);
-        gstore<T, VEC>(d + zstride, o1, c_z, v.n2);
-        gstore<T, VEC>(d + 2 * zstride, o2, c_z, v.n2);
-      }
-    }
+      };
+      if (tile_int && gp >= 2 && gp <= v.n0 - 3) u_items(std::true_type{});
+      else u_items(std::false_type{});
+      lds_barrier();
+      // ---- z' items for plane q = p - 1 (own tile)
+      auto z_items = [&](auto intc) {
+        constexpr bool I = decltype(intc)::value;
+        if (p > p_start && tid < NZ) {
+          const int q = p - 1, gq = gp - 1;
+          const int o = (zi + 1) * WU + 4 * (zg + 1);
+          const G4<T> ua = lds4(&U[sm2][o]), ub = lds4(&U[sm1][o]), uc = lds4(&U[s0][o]);  // u(q-1), u(q), u(q+1)
+          const G4<T> un = lds4(&U[sm1][o - WU]), us = lds4(&U[sm1][o + WU]);             // rows i1-1, i1+1
+          const G4<T> ul = lds4(&U[sm1][o - 4]), ur = lds4(&U[sm1][o + 4]);               // groups left / right
+          const T h2[6] = {ul.v[3], ub.v[0], ub.v[1], ub.v[2], ub.v[3], ur.v[0]};
+          const G4<T> zv0 = lds4(&Z0[sm1][o]);
+          const G4<T> zv1 = lds4(&Z1[b2 ^ 1][(zi + 2) * WU + 4 * (zg + 1)]);
+          const G4<T> zv2 = lds4(&Z2[b2 ^ 1][(zi + 1) * W2 + 4 * (zg + 2)]);
+          const bool own = i1z < v.n1 && gq >= 0 && gq < v.n0 && c_z < v.n2;
+          G4<T> o0, o1, o2;
+          T sdz = T(0), sz = T(0);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int i2 = c_z + m;
+            const bool cm = VEC ? true : (i2 < v.n2);
+            const T w0[5] = {T(0), ua.v[m], ub.v[m], uc.v[m], T(0)};
+            const T w1[5] = {T(0), un.v[m], ub.v[m], us.v[m], T(0)};
+            const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
+            const T k0 = sw_d1_fwd<KK, I>(w0, gq, v.n0, P.inv_step[0], edge);
+            const T k1 = sw_d1_fwd<KK, I>(w1, i1z, v.n1, P.inv_step[1], edge);
+            const T k2 = sw_d1_fwd<KK, I>(w2, i2, v.n2, P.inv_step[2], edge);
+            const T w0v = zv0.v[m] + P.sigma * k0, w1v = zv1.v[m] + P.sigma * k1, w2v = zv2.v[m] + P.sigma * k2;
+            const T v0 = w0v * P.inv_sigma, v1 = w1v * P.inv_sigma, v2 = w2v * P.inv_sigma;
+            T t0, t1, t2;
+            if (hk == PCS_H_L21) {  // w - sigma * (max(1 - t/||v||, 0) v), penalty.py:551-557
+              T f = T(1) - P.t_h * fast_rsqrt(pcs_fma(v0, v0, pcs_fma(v1, v1, v2 * v2)));
+              f = f > T(0) ? f : T(0);
+              t0 = w0v - P.sigma * (f * v0);
+              t1 = w1v - P.sigma * (f * v1);
+              t2 = w2v - P.sigma * (f * v2);
+            } else {  // w - sigma * (v - t*clip(v/t)), func/base.py:239-240
+              t0 = w0v - P.sigma * (v0 - P.t_h * clip1(v0 * P.inv_t_h));
+              t1 = w1v - P.sigma * (v1 - P.t_h * clip1(v1 * P.inv_t_h));
+              t2 = w2v - P.sigma * (v2 - P.t_h * clip1(v2 * P.inv_t_h));
+            }
+            o0.v[m] = pcs_fma(P.rho, t0, P.omr * zv0.v[m]);
+            o1.v[m] = pcs_fma(P.rho, t1, P.omr * zv1.v[m]);
+            o2.v[m] = pcs_fma(P.rho, t2, P.omr * zv2.v[m]);
+            const T e0 = zv0.v[m] - o0.v[m], e1 = zv1.v[m] - o1.v[m], e2 = zv2.v[m] - o2.v[m];
+            sdz += cm ? pcs_fma(e0, e0, pcs_fma(e1, e1, e2 * e2)) : T(0);
+            sz += cm ? pcs_fma(zv0.v[m], zv0.v[m], pcs_fma(zv1.v[m], zv1.v[m], zv2.v[m] * zv2.v[m])) : T(0);
+          }
+          if (own) {
+            part[2] += (double)sdz;
+            part[3] += (double)sz;
+            T* d = zn + (int64_t)(q + v.hz) * pl + (int64_t)i1z * v.n2 + c_z;
+            gstore<T, VEC>(d, o0, c_z, v.n2);
+            gstore<T, VEC>(d + zstride, o1, c_z, v.n2);
+            gstore<T, VEC>(d + 2 * zstride, o2, c_z, v.n2);
+          }
+        }
+      };
+      if (tile_int && gp - 1 >= 2 && gp - 1 <= v.n0 - 3) z_items(std::true_type{});
+      else z_items(std::false_type{});
+  };
+  for (int p = p_start - 1; p <= p_end; p += 2) {
+    iter(p, S0{});
+    if (p + 1 <= p_end) iter(p + 1, S1{});
   }
   block_sum<4>(part, red);
   if (hist != nullptr) {
@@ -596,10 +628,17 @@ struct PlaneBands {
   int64_t a0, b0, a1, b1;
 };
 
+// update-tile rows of the launch: the forward kernel's 8, or the general-K kernel's (k3g_rows)
+static int tile_rows3(const pcs_pds3d_args* a) {
+  if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) return a->dtype == PCS_F32 ? k3g_rows<float>() : k3g_rows<double>();
+  return k3T1;
+}
+
 static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   Plan3 p;
   if (pb.b0 == pb.a0) pb = PlaneBands{pb.a1, pb.b1, pb.b1, pb.b1};
-  p.tiles1 = (int)((a->n1 + k3T1 - 1) / k3T1);
+  const int t1 = tile_rows3(a);
+  p.tiles1 = (int)((a->n1 + t1 - 1) / t1);
   p.tiles2 = (int)((a->n2 + k3TW - 1) / k3TW);
   const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
   const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
@@ -663,7 +702,7 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   }
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
-  static_assert(k3gT1 == k3T1 && k3gTW == k3TW, "the general-K kernel shares the forward kernel's task plan");
+  static_assert(k3gTW == k3TW, "the general-K kernel shares the forward kernel's column tiles");
   if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
     auto kern = a->kkind == PCS_BACKWARD ? k_pds3d_gen<T, PCS_BACKWARD, FK, VEC> : k_pds3d_gen<T, PCS_CENTERED, FK, VEC>;
     kern<<<(unsigned)p.ntasks, k3gNT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g, v,

@@ -24,7 +24,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def build(n, dtype, seed=0):
+def build(n, dtype, seed=0, kind='forward'):
     from pycsou_amd.func.loss import SquaredL2Loss
     from pycsou_amd.func.penalty import L21Norm
     from pycsou_amd.linop.conv import Convolve1D
@@ -51,9 +51,9 @@ def build(n, dtype, seed=0):
     y = C(xs.reshape(-1)) + 0.01 * torch.randn(N, generator=g, device='cuda', dtype=dtype)
     del xs
     print('  blurred data ready', flush=True)
-    K = Gradient(shape=shape, kind='forward')
-    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(sum(4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2
-                                                               for _ in range(3))))
+    K = Gradient(shape=shape, kind=kind)
+    K.lipschitz_cst = K.diff_lipschitz_cst = (float(np.sqrt(sum(4 * np.sin(np.pi * (n - 1) / (2 * n)) ** 2
+                                                                for _ in range(3)))) if kind == 'forward' else 3.0)
     F = (1 / 2) * SquaredL2Loss(dim=N, data=y) * C
     H = 0.05 * L21Norm(dim=3 * N, groups=np.tile(np.arange(N), 3))
     print('  functionals ready', flush=True)
@@ -68,6 +68,7 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=4)
     ap.add_argument('--rank-of', type=int, default=0)
+    ap.add_argument('--kind', default='forward', choices=['forward', 'backward', 'centered'])
     args = ap.parse_args()
     if args.rank_of > 1:
         return rank_share(args)
@@ -75,7 +76,7 @@ def main():
     dtype = torch.float32 if args.dtype == 'f32' else torch.float64
     from pycsou_amd.opt.engine3d import PDS3DEngine
     t0 = time.time()
-    pds = build(args.size, dtype)
+    pds = build(args.size, dtype, kind=args.kind)
     spec = pds._fused_spec()
     assert spec is not None and spec['ndim'] == 3
     chunk = 2
