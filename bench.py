@@ -441,14 +441,13 @@ def leg_c3_nonsep(args, dtype, K, W):
 
 def leg_c3_cen(args, dtype, K, W):
     """The C3 problem with the reference's DEFAULT K = Gradient(shape) (kind='centered', edge=True,
-    pycsou/linop/diff.py:777-778): grad F = N x - Conv^T y with N x = Conv^T Conv x by the in-plane
-    normal-operator kernel (two 29-tap passes, k_sep2d_nrm) into a buffer, then the general-stencil
-    row-marching step (k_pds2d_smarch, SEPCONV: reads x, N x, Conv^T y, z; writes x', z') -- two
-    launches per iteration, back to back from C."""
+    pycsou/linop/diff.py:777-778): grad F = N x - Conv^T y with N = Conv^T Conv as two 29-tap passes
+    inside the row-marching step (the normal-operator march generalised to centred K, one launch per
+    iteration: reads x, Conv^T y, z; writes x', z' -- 7 words, as the forward-K headline kernel); with
+    PCS_NMARCH_GEN=0 the two-launch form (N x by k_sep2d_nrm into a buffer, then the stencil march)."""
     n = args.size
     t0 = time.perf_counter()
     pds = build_problem(n, n, dtype, lipschitz=args.lipschitz, kind='centered')
-    spec = pds._fused_spec()
     setup = time.perf_counter() - t0
     r = fused_2d(pds, dtype, K, W)
     del pds
@@ -456,23 +455,35 @@ def leg_c3_cen(args, dtype, K, W):
     N = n * n
     alg = 7 * N * elem
     km = r['kernels_ms']
-    upd = km['step'] - km.get('conv_nx', 0.0)
-    step_bytes = 8 * N * elem  # the update kernel's own traffic: x, N x, Conv^T y, z (2) in; x', z' (2) out
-    return {'workload': f'C3 TV-deconvolution {n}x{n} {args.dtype}, 15x15 Gaussian PSF (separable), '
-                        f'K = Gradient(shape) (default kind=centered, edge=True), 0.05*L21Norm; grad F = N x - Conv^T y: '
-                        f'N x by k_sep2d_nrm into a buffer + general-stencil march step (k_pds2d_smarch), '
-                        f'two launches per iteration back to back from C',
-            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
-            'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'fkind': r['fkind'],
-            'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
-            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            'roofline': {'bound': 'hbm', 'kernel': 'k_pds2d_smarch<centered, NB, L21> (update)',
-                         'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
-                         'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            'nx_roofline': {'bound': 'lds/fp32-vector', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm)',
-                            'kernel_ms': round(km.get('conv_nx', float('nan')), 5), 'flop_per_launch': 116 * N,
-                            'tflops': round(116 * N / (km.get('conv_nx', float('nan')) * 1e-3) / 1e12, 2)}}
+    two = 'conv_nx' in km
+    res = {'workload': f'C3 TV-deconvolution {n}x{n} {args.dtype}, 15x15 Gaussian PSF (separable), '
+                       f'K = Gradient(shape) (default kind=centered, edge=True), 0.05*L21Norm; grad F = N x - Conv^T y'
+                       + (': N x by k_sep2d_nrm into a buffer + general-stencil march step (k_pds2d_smarch), two '
+                          'launches per iteration' if two else
+                          ', N inside the step (k_pds2d_nmarch_gen<centered>), one launch per iteration')
+                       + ', back to back from C',
+           'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+           'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'fkind': r['fkind'],
+           'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
+           'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if two:
+        upd = km['step'] - km['conv_nx']
+        step_bytes = 8 * N * elem  # the update kernel's own traffic: x, N x, Conv^T y, z (2) in; x', z' (2) out
+        res['roofline'] = {'bound': 'hbm', 'kernel': 'k_pds2d_smarch<centered, NB, L21> (update)',
+                           'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
+                           'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        res['nx_roofline'] = {'bound': 'lds/fp32-vector', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm)',
+                              'kernel_ms': round(km['conv_nx'], 5), 'flop_per_launch': 116 * N,
+                              'tflops': round(116 * N / (km['conv_nx'] * 1e-3) / 1e12, 2)}
+    else:
+        res['roofline'] = {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_nmarch_gen<float,7,L21,256,centered>)',
+                           'kernel_ms': round(km['step'], 5), 'bytes_per_launch': alg,
+                           'achieved': round(alg / (km['step'] * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': round(alg / (km['step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           'conv_flop_per_launch': 116 * N,
+                           'conv_tflops': round(116 * N / (km['step'] * 1e-3) / 1e12, 2)}
+    return res
 
 
 def leg_conv63(args, dtype, K, W):

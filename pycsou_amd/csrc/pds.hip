@@ -210,21 +210,36 @@ template <int H>
 static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p);
 
 // the normal-operator march kernel (pds_nmarch.hpp): fp32 separable tiers 3 / 7 with the host's
-// Conv^T y and N tables; images of at least 64 x 64 (the edge bands of N never overlap)
+// Conv^T y and N tables; images of at least 64 x 64 (the edge bands of N never overlap).  Backward /
+// centred K too (its GEN geometry) unless PCS_NMARCH_GEN=0, when the last strip keeps its column
+// c0 - 1 out of N_h's right edge band (n1 - c0_last > H); else those K take the stencil march
+static bool nmarch_gen_enabled() {
+  const char* e = getenv("PCS_NMARCH_GEN");  // read per call (tests and the A/B switch it)
+  return e == nullptr || atoi(e) != 0;
+}
 static bool use_nmarch(const pcs_pds2d_args* a) {
-  return a->cty != nullptr && a->ntaps != nullptr && aligned16(a->cty) && a->n0 >= 64 && a->n1 >= 64;
+  if (!(a->cty != nullptr && a->ntaps != nullptr && aligned16(a->cty) && a->n0 >= 64 && a->n1 >= 64)) return false;
+  if (a->kkind == PCS_K_GRAD_FORWARD) return true;
+  if (a->kkind != PCS_K_GRAD_BACKWARD && a->kkind != PCS_K_GRAD_CENTERED) return false;
+  const int64_t last = a->n1 - 64 * ((a->n1 + 63) / 64 - 1);  // width of the last 64-column strip
+  return nmarch_gen_enabled() && last > tier_for(a->half);
 }
 
 template <int H>
-static int nmarch_slots() {
-  static int slots = 0;
+static int nmarch_slots(bool gen) {
+  static int slots_f = 0, slots_g = 0;
+  int& slots = gen ? slots_g : slots_f;
   if (slots == 0) {
     int dev = 0, cus = 0, nb = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kNMarchNT>, kNMarchNT,
-                                                     0) != hipSuccess ||
+    const hipError_t oe =
+        gen ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &nb, k_pds2d_nmarch_gen<float, H, PCS_H_L21, kNMarchNT, PCS_CENTERED>, kNMarchNT, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kNMarchNT>,
+                                                           kNMarchNT, 0);
+    if (oe != hipSuccess ||
         nb < 1)
       nb = 3;
     (void)hipGetLastError();
@@ -241,7 +256,7 @@ static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tw = nm ? NMarch<H>::TW : March<H>::TW;
   const int tiles_x = (int)((a->n1 + tw - 1) / tw);
   if (tiles_x < 2) return false;
-  plan_bands(rb, March<H>::TS, tiles_x, nm ? nmarch_slots<H>() : march_slots<H>(), 1, p);
+  plan_bands(rb, March<H>::TS, tiles_x, nm ? nmarch_slots<H>(a->kkind != PCS_K_GRAD_FORWARD) : march_slots<H>(), 1, p);
   return true;
 }
 
@@ -252,6 +267,7 @@ static bool use_march(const pcs_pds2d_args* a) {
   const int t = tier_for(a->half);
   if (a->dtype != PCS_F32 || a->fkind != PCS_F_SEPCONV || (t != 3 && t != 7) || !make_slab(a).vec) return false;
   if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return false;
+  if (a->kkind != PCS_K_GRAD_FORWARD && !use_nmarch(a)) return false;  // only the normal-operator march is general
   const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
                                              : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
   // 32-bit indexing and buffer views of at most 2^30 bytes (pds_march.hpp kOOB)
@@ -268,6 +284,15 @@ static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
+  if (use_nmarch(a) && a->kkind != PCS_K_GRAD_FORWARD) {
+    auto kern = a->kkind == PCS_K_GRAD_BACKWARD ? k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_BACKWARD>
+                                                : k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_CENTERED>;
+    kern<<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn,
+                                                   (const float*)a->cty, (const float*)a->ntaps, s, P, a->gkind,
+                                                   a->edge, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
+                                                   p.tiles_x, p.bd, p.ntasks);
+    return launch_status();
+  }
   if (use_nmarch(a)) {
     k_pds2d_nmarch<float, H, HK, kNMarchNT><<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>(
         (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->cty,
@@ -275,6 +300,7 @@ static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
         p.bd, p.ntasks);
     return launch_status();
   }
+  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
@@ -448,8 +474,12 @@ static bool sm_normal(const pcs_pds2d_args* a) {
                                    nullptr) == PCS_OK;
 }
 
+static bool use_march(const pcs_pds2d_args* a);
+
 static bool use_smarch(const pcs_pds2d_args* a) {
   if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward()) return false;
+  // separable PSF with backward / centred K: the fused normal-operator march (one launch) when it applies
+  if (a->kkind != PCS_K_GRAD_FORWARD && a->fkind == PCS_F_SEPCONV && use_march(a)) return false;
   if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return false;
   if (a->dtype != PCS_F32 || !make_slab(a).vec) return false;
   if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF &&
@@ -531,8 +561,8 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 // the row-marching families (march, pt, smarch) take row bands; the tile kernel runs whole slabs only
 static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   if (use_smarch(a)) return launch_smarch(a, rb, st);
-  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, rb, st) : launch_march<7>(a, rb, st);
+  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, rb, st);
   if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, rb, st);
   return launch_pt<PCS_F_NULL>(a, rb, st);
@@ -540,9 +570,9 @@ static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
-  if (use_smarch(a)) return pds2d_bands(a, full_bands(a), st);
+  if (use_smarch(a) || use_march(a)) return pds2d_bands(a, full_bands(a), st);
   if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
-  if (use_march(a) || use_pt(a)) return pds2d_bands(a, full_bands(a), st);
+  if (use_pt(a)) return pds2d_bands(a, full_bands(a), st);
   switch (a->fkind) {
     case PCS_F_NULL: return launch_pds2d<T, PCS_F_NULL, 0>(a, st);
     case PCS_F_DENOISE: return launch_pds2d<T, PCS_F_DENOISE, 0>(a, st);
@@ -565,12 +595,12 @@ static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb) {
     sm_plan(a, rb, &p);
     return (int64_t)p.ntasks;
   }
-  if (a->kkind != PCS_K_GRAD_FORWARD) return -1;
   if (use_march(a)) {
     if (tier_for(a->half) == 3) march_plan<3>(a, rb, &p);
     else march_plan<7>(a, rb, &p);
     return (int64_t)p.ntasks;
   }
+  if (a->kkind != PCS_K_GRAD_FORWARD) return -1;
   if (use_pt(a)) {
     pt_plan(a, rb, &p);
     return (int64_t)p.ntasks;
@@ -687,7 +717,7 @@ int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int6
   if (rc != PCS_OK) return rc;
   if (a->hist || !bands_ok(a, ra0, rb0, ra1, rb1)) return PCS_EINVAL;
   if (a->fkind == PCS_F_CONV2D) return PCS_EUNSUPPORTED;  // its correlation passes run once per iteration
-  if (!(use_smarch(a) || (a->kkind == PCS_K_GRAD_FORWARD && (use_march(a) || use_pt(a))))) return PCS_EUNSUPPORTED;
+  if (!(use_smarch(a) || use_march(a) || (a->kkind == PCS_K_GRAD_FORWARD && use_pt(a)))) return PCS_EUNSUPPORTED;
   return pds2d_bands(a, RowBands{ra0, rb0, ra1, rb1}, st);
 }
 
@@ -697,7 +727,7 @@ int pcs_pds2d_supported(const pcs_pds2d_args* a) {
     const pcs_pds2d_args b = step_args(a);
     return pcs_pds2d_supported(&b);
   }
-  if (a->kkind != PCS_K_GRAD_FORWARD) return use_smarch(a) ? 1 : 0;
+  if (a->kkind != PCS_K_GRAD_FORWARD) return (use_smarch(a) || use_march(a)) ? 1 : 0;
   if (use_smarch(a) || use_march(a) || use_pt(a)) return 1;
   return (a->dtype == PCS_F32 || a->dtype == PCS_F64) && (a->fkind != PCS_F_SEPCONV || tier_for(a->half) > 0) ? 1 : 0;
 }

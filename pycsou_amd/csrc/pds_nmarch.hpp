@@ -48,7 +48,10 @@
 #define PCS_NM_SAUX 16
 #endif
 
+#include <type_traits>
+
 #include "pds_march.hpp"
+#include "stencil.hpp"
 
 namespace pcs {
 
@@ -86,7 +89,16 @@ __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int H>
+// diagnostics builds (timing only, wrong results): 1 = GEN without its extra columns, 2 = GEN with
+// interior stencils everywhere, 4 = the forward kernel without its 65th column
+#ifndef PCS_NMG_ABL
+#define PCS_NMG_ABL 0
+#endif
+// GEN: backward / centred K (KK != PCS_FORWARD) -- K^T z reads z rows lr - 1 .. lr + 1 and columns
+// c - 1 .. c + 1, K u reads u rows r - 1 .. r + 1 and columns c - 1 .. c + 1: z tiles of 18 rows (the
+// z0 tile from column c0 - 4 too), an 18-row u ring, and a sixth u / t / g column c0 - 1 (group 0,
+// slot SLM1 of the t and u rows) beside the 65th
+template <int H, bool GEN = false>
 struct NMarch {
   static constexpr int TW = 64, TS = 16, NQ = 4 * H + 1;
   static constexpr int XL = RU4<2 * H>::value, SHX = XL - 2 * H;  // x region [c0 - XL, c0 + TW + XL)
@@ -95,16 +107,20 @@ struct NMarch {
   // t ring: 48 rows (a step's window + new rows: 4H + 2 TS <= 48 + TS) + a mirror of its first 4H
   // (rows 48..48+4H-1 repeat rows 0..4H-1), so any (4H+1)-row window starting in the ring is contiguous
   static constexpr int XRING = 32, TRING = 48, TMIR = 4 * H;
-  static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B)
-  // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 16 groups, z1 rows
-  // of 17 groups (from column c0 - 4); 5 wave-instructions of 64 x 16 B each
-  static constexpr int WZ0 = TW + 4, WZ1 = TW + 8, ZSLOTS = 5 * 64;
+  static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B; GEN: 66)
+  static constexpr int SLM1 = TW + 1;             // GEN: slot of column c0 - 1 in a t / u row
+  // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 17 groups (from
+  // column c0; GEN: 18 from c0 - 4), z1 rows of 18 groups (from column c0 - 4); ZR rows from row a;
+  // 5 (GEN: 6) wave-instructions of 64 x 16 B each
+  static constexpr int ZR = GEN ? TS + 2 : TS + 1, Z0C = GEN ? 4 : 0, Z0G = GEN ? 18 : 17;
+  static constexpr int WZ0 = 4 * Z0G, WZ1 = TW + 8, ZSLOTS = (GEN ? 6 : 5) * 64;
+  static constexpr int UR = GEN ? TS + 2 : TS + 1;  // u ring rows: [a, a+16] (GEN: [a-1, a+16])
   static constexpr int NVH = (SHX + 3 + 4 * H) / 4 + 1;  // b128 groups a PH item reads
   static constexpr int NXN = TS * GXL;                   // x items per step
-  static constexpr int NXP = (4 * H + 1) * GXL;          // prologue x items
-  static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + (TRING + TMIR) * WT, O_W = O_U + (TS + 1) * WU,
+  static constexpr int NXP = (4 * H + 1 + (GEN ? 1 : 0)) * GXL;  // prologue x items
+  static constexpr int O_XR = 0, O_T = O_XR + XRING * WX, O_U = O_T + (TRING + TMIR) * WT, O_W = O_U + UR * WU,
                        NW = 64 + 32 * H, SZ = O_W + NW;  // W: the ntaps table
-  static_assert((TS + 1) * (WZ0 / 4) <= ZSLOTS && (TS + 1) * (WZ1 / 4) <= ZSLOTS, "z tiles");
+  static_assert(ZR * (WZ0 / 4) <= ZSLOTS && ZR * (WZ1 / 4) <= ZSLOTS, "z tiles");
   static_assert(H == 3 || H == 7, "tiers 3 and 7");
   static_assert(TS + 2 * H + 1 + TS <= XRING + 1 + 2 * H, "x ring holds rows [a+1, a+2H+17)");
   static_assert(4 * H + TS <= TRING, "t ring holds a step's PV window (the rows PH writes are its newest)");
@@ -113,15 +129,18 @@ struct NMarch {
   static_assert((WX / 4) % 2 == 1, "odd x slot pitch");
 };
 
-template <typename T, int H, int HK, int NT>
+template <typename T, int H, int HK, int NT, int KK>
 __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z,
                                             T* __restrict__ zn, const T* __restrict__ b,
                                             const T* __restrict__ tq, const Slab32& s, const Params<T>& P, int gk,
-                                            int s0, int s1, int c0, T* sm, T* Z0, T* Z1, double (&part)[4]) {
+                                            int edge, int s0, int s1, int c0, T* sm, T* Z0, T* Z1,
+                                            double (&part)[4]) {
   static_assert(sizeof(T) == 4 && NT == 256, "fp32, 256 threads (4 rows x 16 column groups per wave)");
-  using M = NMarch<H>;
+  constexpr bool GEN = KK != PCS_FORWARD;
+  using M = NMarch<H, GEN>;
   constexpr int TS = M::TS, TW = M::TW, NQ = M::NQ, XL = M::XL, SHX = M::SHX, NVH = M::NVH;
   constexpr int WX = M::WX, WT = M::WT, WU = M::WU, WZ0 = M::WZ0, WZ1 = M::WZ1, GXL = M::GXL;
+  constexpr int UR = M::UR, ZR = M::ZR, SLM1 = M::SLM1;
   constexpr int KXN = cdiv(M::NXN, NT), KXP = cdiv(M::NXP, NT);
   constexpr int GG = TW / 4;
   T* XR = sm + M::O_XR;
@@ -152,6 +171,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   const bool cin = ucg < n1;                        // group in the image (4-groups wholly in / out)
   const bool clast = ucg == n1 - 4;                 // holds the image's last column
   const bool cown = cin;                            // stored by this workgroup
+  // GEN: the strip's columns c0 - 1 .. c0 + 64 >= 2 samples inside the image (no column edge rules)
+  const bool cint = c0 >= 4 && c0 + TW + 3 <= n1 - 3;
   uint32_t co_xn[KXN];
   int rr_xn[KXN];
 #pragma unroll
@@ -174,22 +195,23 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       st4(XR + ((r0 + r) & 31) * WX + 4 * g, xv[k]);
     }
   };
-  // z0 rows [a, a + TS], cols [c0, c0 + TW + 4) -> Z0; z1 rows [a, a + TS], cols [c0 - 4, c0 + TW + 4) -> Z1,
+  // z0 rows [a, a + ZR), cols [c0 - Z0C, c0 + TW + 4) -> Z0; z1 rows [a, a + ZR), cols [c0 - 4, c0 + TW + 4) -> Z1,
   // straight into LDS (buffer_load ... lds: no VGPRs, no ds_write).  Wave w issues tile
-  // instructions w and w + 4 of each tile (5 each): lane l of instruction j fills slot 64 j + l (rows past
-  // the tile and rows below `rmin` read as 0).  The issuing waves wait for them (vmcnt) before the
+  // instructions w and w + 4 of each tile (5 / 6 each): lane l of instruction j fills slot 64 j + l (rows
+  // past the tile and rows below `rmin` read as 0).  The issuing waves wait for them (vmcnt) before the
   // barrier that precedes the first read.
   const int lane = tid & 63;
   auto load_z = [&](int a, int rmin) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wv + 4 * jj;
-      if (j < 5) {
+      if (j < M::ZSLOTS / 64) {
         const int e = 64 * j + lane;
-        const int r0 = e / 17, g0 = e - 17 * (e / 17);  // z0: 17 groups per row (cols c0 .. c0 + 67)
+        constexpr int G0 = M::Z0G;
+        const int r0 = e / G0, g0 = e - G0 * (e / G0);  // z0: 17 (GEN: 18) groups per row
         const int r1 = e / 18, g1 = e - 18 * (e / 18);  // z1: 18 groups per row (cols c0 - 4 .. c0 + 67)
-        const uint32_t o0 = (r0 > TS || r0 < rmin ? kOOB : vz0.row_off(a + r0)) + col_off(c0 + 4 * g0, n1);
-        const uint32_t o1 = (r1 > TS || r1 < rmin ? kOOB : vz1.row_off(a + r1)) + col_off(c0 - 4 + 4 * g1, n1);
+        const uint32_t o0 = (r0 >= ZR || r0 < rmin ? kOOB : vz0.row_off(a + r0)) + col_off(c0 - M::Z0C + 4 * g0, n1);
+        const uint32_t o1 = (r1 >= ZR || r1 < rmin ? kOOB : vz1.row_off(a + r1)) + col_off(c0 - 4 + 4 * g1, n1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vz0.r, (__attribute__((address_space(3))) void*)(Z0 + 256 * j), 16,
                                                  o0, 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vz1.r, (__attribute__((address_space(3))) void*)(Z1 + 256 * j), 16,
@@ -209,7 +231,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       for (int e = 0; e < 4; ++e) v[4 * q + e] = t4.v[e];
     }
     G4<T> o;
-    T o4 = T(0);
+    T o4 = T(0), om1 = T(0);  // om1 (GEN): column c0 - 1 (kept by group 0)
 #pragma unroll
     for (int m = 0; m < 4; ++m) o.v[m] = T(0);
     // taps 4 at a time (broadcast LDS reads), the next 4 read while the current ones are used
@@ -226,10 +248,12 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #pragma unroll
           for (int m = 0; m < 4; ++m) o.v[m] += wc.v[e] * v[SHX + m + q];
           o4 += wc.v[e] * v[SHX + 4 + q];
+          if constexpr (GEN) om1 += wc.v[e] * v[SHX - 1 + q];
         }
       }
       pin4(o);
       pin1(o4);
+      if constexpr (GEN) pin1(om1);
       pcs_fence();
       wc = wn;
     }
@@ -265,17 +289,25 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     T* trow = TR + sl * WT + 4 * ug;
     st4(trow, o);
     if (ug == GG - 1) trow[4] = o4;
+    if constexpr (GEN) {  // column c0 - 1 (>= H columns inside the image, or outside it: no edge rows of N_h)
+      if (ug == 0) trow[SLM1] = om1;
+    }
     if (sl < M::TMIR) {  // the mirror copy
       st4(trow + M::TRING * WT, o);
       if (ug == GG - 1) trow[M::TRING * WT + 4] = o4;
+      if constexpr (GEN) {
+        if (ug == 0) trow[M::TRING * WT + SLM1] = om1;
+      }
     }
   };
   // ---- PV + update: row lr = a + 1 + ui, columns [c, c + 4); the last group also column c + 4
   // (the strip's 65th), in a branch of its own lanes (4 per wave: conflict-free b32 reads)
-  auto pv = [&](int a, const G4<T>& bv, T b5, int ub) {
+  auto pv = [&](int a, const G4<T>& bv, T b5, T bm1, int ub) {
     const int lr = a + 1 + ui, gr = s.row0 + lr;
+    // GEN: the step's update rows [a+1, a+16] and z' rows [a, a+16) >= 2 samples inside the image
+    const bool rint = s.row0 + a >= 2 && s.row0 + a + TS <= n0 - 3;
     int slot = ui + 1 + ub;
-    slot = slot >= 17 ? slot - 17 : slot;
+    slot = slot >= UR ? slot - UR : slot;
     // g = N_v t - b: rows lr - 2H .. lr + 2H of the t ring, window row q at p0 + q rows (no
     // address arithmetic: immediate offsets); reads are issued in chunks of PF behind a compiler
     // fence (at most 2 PF in flight)
@@ -325,65 +357,140 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
         for (int m = 0; m < 4; ++m) g.v[m] -= w * t4.v[m];
       }
     }
-    const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
-    const G4<T> za = lds4(Z0 + ui * WZ0 + 4 * ug);               // z0[lr - 1]
-    const G4<T> zb = lds4(Z0 + (ui + 1) * WZ0 + 4 * ug);         // z0[lr]
-    const G4<T> z1a = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug);        // z1[lr][c - 4 .. c - 1]
-    const G4<T> z1b = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug + 4);    // z1[lr][c .. c + 3]
-    const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
-    const bool rrow = gr < n0 && lr <= s.rows;
-    const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
-    // x_t = prox_G((x - tau g) - tau K^T z); K^T z for forward differences, VStack order:
-    // (0 + D0^T z0) + D1^T z1
-    auto xt_of = [&](T gd, T xv, T za_, T zb_, T zl, T zr, bool last_col) {
-      T d0 = r_first ? T(0) : za_;
-      if (!r_last) d0 -= zb_;
-      const T d1 = zl - (last_col ? T(0) : zr);
-      return prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
-    };
-    G4<T> uo, xo;
-    T sdx = T(0), sx = T(0);
+    if constexpr (!GEN) {
+      const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
+      const G4<T> za = lds4(Z0 + ui * WZ0 + 4 * ug);               // z0[lr - 1]
+      const G4<T> zb = lds4(Z0 + (ui + 1) * WZ0 + 4 * ug);         // z0[lr]
+      const G4<T> z1a = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug);        // z1[lr][c - 4 .. c - 1]
+      const G4<T> z1b = lds4(Z1 + (ui + 1) * WZ1 + 4 * ug + 4);    // z1[lr][c .. c + 3]
+      const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
+      const bool rrow = gr < n0 && lr <= s.rows;
+      const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+      // x_t = prox_G((x - tau g) - tau K^T z); K^T z for forward differences, VStack order:
+      // (0 + D0^T z0) + D1^T z1
+      auto xt_of = [&](T gd, T xv, T za_, T zb_, T zl, T zr, bool last_col) {
+        T d0 = r_first ? T(0) : za_;
+        if (!r_last) d0 -= zb_;
+        const T d1 = zl - (last_col ? T(0) : zr);
+        return prox_g((xv - P.tau * gd) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a, P.seg_b);
+      };
+      G4<T> uo, xo;
+      T sdx = T(0), sx = T(0);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const T xv = xv4.v[m];
-      const T xt = xt_of(g.v[m] - bv.v[m], xv, za.v[m], zb.v[m], (m == 0) ? z1a.v[3] : z1b.v[m - 1], z1b.v[m],
-                         m == 3 && clast);
-      uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
-      const T xnew = P.rho * xt + P.omr * xv;
-      xo.v[m] = xnew;
-      const T dx = xv - xnew;
-      sdx += dx * dx;
-      sx += xv * xv;
-    }
-    if (own) {
-      part[0] += (double)sdx;
-      part[1] += (double)sx;
-    }
-    T* urow = U + slot * WU + 4 * ug;
-    st4(urow, uo);
-    bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
-    if (ug == GG - 1) {  // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0)
-      const T* q0 = p0 + 4;
-      T g4 = T(0);
-#pragma unroll
-      for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {
-        const G4<T> w = lds4(Wq + 4 * q4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (4 * q4 + e < NQ) g4 += w.v[e] * lds1(q0 + (4 * q4 + e) * WT);
+      for (int m = 0; m < 4; ++m) {
+        const T xv = xv4.v[m];
+        const T xt = xt_of(g.v[m] - bv.v[m], xv, za.v[m], zb.v[m], (m == 0) ? z1a.v[3] : z1b.v[m - 1], z1b.v[m],
+                           m == 3 && clast);
+        uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
+        const T xnew = P.rho * xt + P.omr * xv;
+        xo.v[m] = xnew;
+        const T dx = xv - xnew;
+        sdx += dx * dx;
+        sx += xv * xv;
       }
-      if (vedge) {
-#pragma unroll
-        for (int k = 0; k < H; ++k) g4 -= ((top || bot) ? d[k] : T(0)) * lds1(TR + (M::tslot(kr0) + k) * WT + TW);
+      if (own) {
+        part[0] += (double)sdx;
+        part[1] += (double)sx;
       }
-      const T xe = lds1(XR + (lr & 31) * WX + XL + TW);
-      const T xt = xt_of(g4 - b5, xe, lds1(Z0 + ui * WZ0 + TW), lds1(Z0 + (ui + 1) * WZ0 + TW), z1b.v[3],
-                         lds1(Z1 + (ui + 1) * WZ1 + TW + 4), false);
-      urow[4] = (rrow && ucg + 4 < n1) ? (T(2) * xt - xe) : T(0);
+      T* urow = U + slot * WU + 4 * ug;
+      st4(urow, uo);
+      bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+      if (!(PCS_NMG_ABL & 4) && ug == GG - 1) {  // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0)
+        const T* q0 = p0 + 4;
+        T g4 = T(0);
+#pragma unroll
+        for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {
+          const G4<T> w = lds4(Wq + 4 * q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q4 + e < NQ) g4 += w.v[e] * lds1(q0 + (4 * q4 + e) * WT);
+        }
+        if (vedge) {
+#pragma unroll
+          for (int k = 0; k < H; ++k) g4 -= ((top || bot) ? d[k] : T(0)) * lds1(TR + (M::tslot(kr0) + k) * WT + TW);
+        }
+        const T xe = lds1(XR + (lr & 31) * WX + XL + TW);
+        const T xt = xt_of(g4 - b5, xe, lds1(Z0 + ui * WZ0 + TW), lds1(Z0 + (ui + 1) * WZ0 + TW), z1b.v[3],
+                           lds1(Z1 + (ui + 1) * WZ1 + TW + 4), false);
+        urow[4] = (rrow && ucg + 4 < n1) ? (T(2) * xt - xe) : T(0);
+      }
+    } else {  // backward / centred K: K^T z from z rows lr - 1 .. lr + 1, columns c - 1 .. c + 1
+      const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
+      const T* z0p = Z0 + ui * WZ0 + 4 * ug + 4;  // tile row ui = row lr - 1, column c
+      const G4<T> za = lds4(z0p), zb = lds4(z0p + WZ0), zc = lds4(z0p + 2 * WZ0);
+      const T* z1p = Z1 + (ui + 1) * WZ1 + 4 * ug;  // row lr, columns c - 4 ..
+      const G4<T> z1a = lds4(z1p), z1b = lds4(z1p + 4);
+      const T z1r = lds4(z1p + 8).v[0];
+      const T zh[6] = {z1a.v[3], z1b.v[0], z1b.v[1], z1b.v[2], z1b.v[3], z1r};
+      const bool rrow = (unsigned)gr < (unsigned)n0 && lr <= s.rows;
+      const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+      // x_t = prox_G((x - tau (g - b)) - tau K^T z), K^T z = D0^T z0 + D1^T z1 (stencil.hpp windows;
+      // I: rows and columns >= 2 samples inside the image, no edge rules -- the same bits)
+      auto xt_of = [&](auto intc, T gd, T xv, const T (&w0)[5], const T (&w1)[5], int i1) {
+        constexpr bool I = decltype(intc)::value || (PCS_NMG_ABL & 2);
+        const T kt = pcs_fma(sw_d1_adj<KK, I>(w0, gr, n0, edge), P.inv_step0,
+                             sw_d1_adj<KK, I>(w1, i1, n1, edge) * P.inv_step1);
+        return prox_g((xv - P.tau * gd) - P.tau * kt, gk, P.seg_a, P.seg_b);
+      };
+      G4<T> uo, xo;
+      T sdx = T(0), sx = T(0);
+      auto items = [&](auto intc) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const T xv = xv4.v[m];
+          const T w0[5] = {T(0), za.v[m], zb.v[m], zc.v[m], T(0)};
+          const T w1[5] = {T(0), zh[m], zh[m + 1], zh[m + 2], T(0)};
+          const T xt = xt_of(intc, g.v[m] - bv.v[m], xv, w0, w1, ucg + m);
+          uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
+          const T xnew = pcs_fma(P.rho, xt, P.omr * xv);
+          xo.v[m] = xnew;
+          const T dx = xv - xnew;
+          sdx += dx * dx;
+          sx += xv * xv;
+        }
+      };
+      if (rint && cint) items(std::true_type{});
+      else items(std::false_type{});
+      if (own) {
+        part[0] += (double)sdx;
+        part[1] += (double)sx;
+      }
+      T* urow = U + slot * WU + 4 * ug;
+      st4(urow, uo);
+      bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+      // the two extra columns in ONE branch of the lanes that hold them (group 0: c0 - 1, >= H inside
+      // the image or outside it; the last group: c0 + 64, < n1 - H or the image's last group), with
+      // per-lane column / slot / tile index: the wave runs the vertical 4H+1-tap pass once, not twice
+      if (!(PCS_NMG_ABL & 1) && (ug == 0 || ug == GG - 1)) {
+        const bool left = ug == 0;
+        const int col = left ? c0 - 1 : c0 + TW, ts = left ? SLM1 : TW, ti = left ? 3 : TW + 4;
+        const T* q0 = TR + M::tslot(lr - 2 * H) * WT + ts;
+        T tv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) tv[q] = q0[q * WT];  // plain reads: issued together, then the FMAs
+        T gx = T(0);
+#pragma unroll
+        for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {
+          const G4<T> w = lds4(Wq + 4 * q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q4 + e < NQ) gx += w.v[e] * tv[4 * q4 + e];
+        }
+        if (vedge) {
+#pragma unroll
+          for (int k = 0; k < H; ++k) gx -= ((top || bot) ? d[k] : T(0)) * TR[(M::tslot(kr0) + k) * WT + ts];
+        }
+        const T xe = XR[(lr & 31) * WX + XL + (col - c0)];
+        const T w0[5] = {T(0), Z0[ui * WZ0 + ti], Z0[(ui + 1) * WZ0 + ti], Z0[(ui + 2) * WZ0 + ti], T(0)};
+        const T* z1e = Z1 + (ui + 1) * WZ1 + ti;
+        const T w1[5] = {T(0), z1e[-1], z1e[0], z1e[1], T(0)};
+        const T xt = xt_of(std::false_type{}, gx - (left ? bm1 : b5), xe, w0, w1, col);
+        U[slot * WU + ts] = (rrow && (unsigned)col < (unsigned)n1) ? (T(2) * xt - xe) : T(0);
+      }
     }
   };
   // ---- P6: z' on row lr = a + ui
-  auto p6 = [&](int a, int ub) {
+  auto p6f = [&](int a, int ub) {
     const int lr = a + ui, gr = s.row0 + lr;
     int sl0 = ui + ub, sl1 = ui + 1 + ub;
     sl0 = sl0 >= 17 ? sl0 - 17 : sl0;
@@ -427,44 +534,115 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     bstore4<PCS_NM_SAUX>(rzn0, off, o0);
     bstore4<PCS_NM_SAUX>(rzn1, off, o1);
   };
+  // ---- P6 (GEN): z' on row lr = a + ui; K u from u rows lr - 1 .. lr + 1 (ring rows [a - 1, a + 16]) and
+  // columns c - 1 .. c + 4 (c0 - 1 at SLM1, c0 + 64 at slot TW)
+  auto p6g = [&](int a, int ub) {
+    const int lr = a + ui, gr = s.row0 + lr;
+    int slm = ui - 1 + ub, sl0 = ui + ub, sl1 = ui + 1 + ub;
+    slm = slm < 0 ? slm + UR : (slm >= UR ? slm - UR : slm);
+    sl0 = sl0 >= UR ? sl0 - UR : sl0;
+    sl1 = sl1 >= UR ? sl1 - UR : sl1;
+    const T* u0 = U + sl0 * WU;
+    const G4<T> uc = lds4(u0 + 4 * ug), ud = lds4(U + sl1 * WU + 4 * ug), uu = lds4(U + slm * WU + 4 * ug);
+    const T ur4 = lds4(u0 + 4 * ug + 4).v[0];               // u[c + 4] (a b128 read: conflict-free)
+    const T ul = lds1(u0 + (ug == 0 ? SLM1 : 4 * ug - 1));  // u[c - 1]
+    const T uh[6] = {ul, uc.v[0], uc.v[1], uc.v[2], uc.v[3], ur4};
+    const G4<T> zv0 = lds4(Z0 + ui * WZ0 + 4 * ug + 4);
+    const G4<T> zv1 = lds4(Z1 + ui * WZ1 + 4 * ug + 4);
+    const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
+    const bool rint = s.row0 + a >= 2 && s.row0 + a + TS <= n0 - 3;
+    G4<T> o0, o1;
+    T sdz = T(0), sz = T(0);
+    auto items = [&](auto intc) {
+      constexpr bool I = decltype(intc)::value || (PCS_NMG_ABL & 2);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const T w0[5] = {T(0), uu.v[m], uc.v[m], ud.v[m], T(0)};
+        const T w1[5] = {T(0), uh[m], uh[m + 1], uh[m + 2], T(0)};
+        const T k0 = sw_d1_fwd<KK, I>(w0, gr, n0, P.inv_step0, edge);
+        const T k1 = sw_d1_fwd<KK, I>(w1, ucg + m, n1, P.inv_step1, edge);
+        const T w0v = zv0.v[m] + P.sigma * k0, w1v = zv1.v[m] + P.sigma * k1;
+        T zt0, zt1;
+        if (HK == PCS_H_L21) {  // w min(1, lam / ||w||), as p6f
+          const T sc = fminf(T(1), P.lam * fast_rsqrt(pcs_fma(w0v, w0v, w1v * w1v)));
+          zt0 = w0v * sc;
+          zt1 = w1v * sc;
+        } else {
+          zt0 = fminf(fmaxf(w0v, -P.lam), P.lam);
+          zt1 = fminf(fmaxf(w1v, -P.lam), P.lam);
+        }
+        o0.v[m] = pcs_fma(P.rho, zt0, P.omr * zv0.v[m]);
+        o1.v[m] = pcs_fma(P.rho, zt1, P.omr * zv1.v[m]);
+        const T e0 = zv0.v[m] - o0.v[m], e1 = zv1.v[m] - o1.v[m];
+        sdz += pcs_fma(e0, e0, e1 * e1);
+        sz += pcs_fma(zv0.v[m], zv0.v[m], zv1.v[m] * zv1.v[m]);
+      }
+    };
+    if (rint && cint) items(std::true_type{});
+    else items(std::false_type{});
+    if (own) {
+      part[2] += (double)sdz;
+      part[3] += (double)sz;
+    }
+    const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_u;
+    bstore4<PCS_NM_SAUX>(rzn0, off, o0);
+    bstore4<PCS_NM_SAUX>(rzn1, off, o1);
+  };
+  auto p6 = [&](int a, int ub) {
+    if constexpr (GEN) p6g(a, ub);
+    else p6f(a, ub);
+  };
 
-  // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0
-  // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5)
+  // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0 (GEN: t rows from s0 - 2H - 1,
+  // u on rows s0 - 1 and s0)
+  // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5; GEN:
+  // group 0 also column c0 - 1, bm1)
   const uint32_t co_b5 = ug == GG - 1 ? col_off(c0 + TW, n1) : kOOB;
+  const uint32_t co_bm1 = (GEN && ug == 0) ? col_off(c0 - 4, n1) : kOOB;
+  constexpr int PR = GEN ? 1 : 0;  // extra prologue rows
   G4<T> xnx[KXN], bv;
-  T b5;
+  T b5, bm1 = T(0);
   {
     G4<T> xv[KXP];
 #pragma unroll
     for (int k = 0; k < KXP; ++k) {
       const int e = PCS_ITEM(k, M::NXP);
       const int r = e / GXL, g = e - (e / GXL) * GXL;
-      xv[k] = bload4(vx.r, vx.row_off(s0 - 2 * H + r) + col_off(xc0 + 4 * g, n1));
+      xv[k] = bload4(vx.r, vx.row_off(s0 - 2 * H - PR + r) + col_off(xc0 + 4 * g, n1));
     }
-    load_z(s0 - TS, TS - 1);  // z rows s0 - 1, s0 only (the prologue's one update row), b on row s0
-    bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
-    b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
+    // z rows s0 - 1, s0 only (GEN: s0 - 3 .. s0 + 1) for the prologue's update rows; b on those rows
+    load_z(s0 - TS, GEN ? TS - 3 : TS - 1);
+    if constexpr (GEN) {  // rows s0 - 1 (ui 14) and s0 (ui 15)
+      const uint32_t rbp = ui >= TS - 2 ? vb.row_off(s0 - TS + 1 + ui) : kOOB;
+      bv = bload4(vb.r, rbp + co_u);
+      b5 = bload4(vb.r, rbp + co_b5).v[0];
+      bm1 = bload4(vb.r, rbp + co_bm1).v[3];
+    } else {
+      bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
+      b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
+    }
 #pragma unroll
     for (int k = 0; k < KXP; ++k) {
       if (!PCS_WAVE_ON(k, M::NXP)) continue;
       const int e = PCS_ITEM(k, M::NXP);
       const int r = e / GXL, g = e - (e / GXL) * GXL;
-      st4(XR + ((s0 - 2 * H + r) & 31) * WX + 4 * g, xv[k]);
+      st4(XR + ((s0 - 2 * H - PR + r) & 31) * WX + 4 * g, xv[k]);
     }
     vm_wait<0>();
   }
   lds_barrier();
-  ph(s0 - 2 * H + ui);  // t rows [s0 - 2H, s0 - 2H + 16)
-  if (ui + TS < 4 * H + 1) ph(s0 - 2 * H + TS + ui);  // t rows [s0 - 2H + 16, s0 + 2H]
+  ph(s0 - 2 * H - PR + ui);  // t rows [s0 - 2H - PR, s0 - 2H - PR + 16)
+  if (ui + TS < 4 * H + 1 + PR) ph(s0 - 2 * H - PR + TS + ui);  // t rows [.. + 16, s0 + 2H]
   lds_barrier();
-  if (wv == 3) pv(s0 - TS, bv, b5, 1);  // u on row s0 -> u ring slot 0, x' on row s0 (rows above: not own)
+  // u on row s0 (GEN: s0 - 1 too) -> the ring slots of step 0's rows a - 1, a; x' on row s0 (rows above: not own)
+  if (wv == 3) pv(s0 - TS, bv, b5, bm1, UR - TS);
   load_xn(xnx, s0 + 2 * H + 1);        // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
   lds_barrier();
   store_xn(xnx, s0 + 2 * H + 1);  // slots of rows [s0 + 2H - 31, s0 + 2H - 15): read by PH above only
 
   // ================= march: step k covers t rows [a+2H+1, a+2H+17), u / x' rows [a+1, a+17), z' rows [a, a+16)
   const int nsteps = (s1 - s0 + TS - 1) / TS;
-  int ub = 0;  // (-k) mod 17: row r = a + j sits in u ring slot (j + ub) mod 17
+  int ub = 0;  // (16 k) mod UR: row r = a + j sits in u ring slot (j + ub) mod UR
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
     lds_barrier();  // step k-1 done with U, Z and the t / x ring rows it read; its x rows landed
@@ -478,31 +656,34 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     const uint32_t rb = vb.row_off(a + 1 + ui);
     bv = bload4(vb.r, rb + co_u);
     b5 = bload4(vb.r, rb + co_b5).v[0];
+    if constexpr (GEN) bm1 = bload4(vb.r, rb + co_bm1).v[3];
     load_xn(xnx, a + 2 * H + 1 + TS);
 #if PCS_NM_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
     ph(a + 2 * H + 1 + ui);
-    vm_wait<KXN + 2>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
+    vm_wait<KXN + 2 + PR>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
-    pv(a, bv, b5, ub);
+    pv(a, bv, b5, bm1, ub);
     lds_barrier();
     p6(a, ub);
     store_xn(xnx, a + 2 * H + 1 + TS);  // x ring slots of rows [a + 2H - 15, a + 2H + 1): read above
-    ub = ub == 0 ? 16 : ub - 1;
+    if constexpr (GEN) ub = ub + TS >= UR ? ub + TS - UR : ub + TS;
+    else ub = ub == 0 ? 16 : ub - 1;
   }
 #undef PCS_WAVE_ON
 #undef PCS_ITEM
 }
 
 // One block per task (64-column strip x row segment); with `hist` the last workgroups also
-// reduce the partials and run the loop control, with `ro.sums` they only reduce.
+// reduce the partials and run the loop control, with `ro.sums` they only reduce.  The C3 kernel
+// (forward K):
 template <typename T, int H, int HK, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))) void k_pds2d_nmarch(
     const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
     const T* __restrict__ b, const T* __restrict__ tq, Slab32 s, Params<T> P, int gk, double* __restrict__ partials,
     Ctrl* ctrl, double* hist, void* ws, RedOut ro, int tiles_x, Bands bd, int ntasks) {
-  using M = NMarch<H>;
+  using M = NMarch<H, false>;
   __shared__ __attribute__((aligned(16))) T sm[M::SZ];
   __shared__ __attribute__((aligned(16))) T zs0[4 * M::ZSLOTS];  // z tiles: own arrays, so the LDS-DMA
   __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];  // into them never aliases a ring read
@@ -522,7 +703,45 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  if (!stopped) nmarch_task<T, H, HK, NT>(x, xn, z, zn, b, tq, s, P, gk, s0, s1, c0, sm, zs0, zs1, part);
+  if (!stopped) nmarch_task<T, H, HK, NT, PCS_FORWARD>(x, xn, z, zn, b, tq, s, P, gk, 0, s0, s1, c0, sm, zs0, zs1, part);
+  block_sum<4>(part, red);
+  if (hist != nullptr || ro.sums != nullptr) {
+    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
+  } else if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
+  }
+}
+
+// backward / centred K (KK; `edge` = Gradient(edge=...) of the centred kind): the GEN geometry
+template <typename T, int H, int HK, int NT, int KK>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))) void k_pds2d_nmarch_gen(
+    const T* __restrict__ x, T* __restrict__ xn, const T* __restrict__ z, T* __restrict__ zn,
+    const T* __restrict__ b, const T* __restrict__ tq, Slab32 s, Params<T> P, int gk, int edge,
+    double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
+    int ntasks) {
+  static_assert(KK == PCS_BACKWARD || KK == PCS_CENTERED, "k_pds2d_nmarch is the forward kernel");
+  using M = NMarch<H, true>;
+  __shared__ __attribute__((aligned(16))) T sm[M::SZ];
+  __shared__ __attribute__((aligned(16))) T zs0[4 * M::ZSLOTS];
+  __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];
+  __shared__ double red[4 * (NT / 64)];
+  __shared__ int flag[2];
+  const bool stopped = stop_requested(ctrl, ro, flag);
+  if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
+
+  int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
+  {
+    const int bb = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
+    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int seg = task / tiles_x, strip = task - seg * tiles_x;
+  int s0, s1;
+  band_rows(bd, seg, s0, s1);
+  const int c0 = strip * M::TW;
+
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  if (!stopped) nmarch_task<T, H, HK, NT, KK>(x, xn, z, zn, b, tq, s, P, gk, edge, s0, s1, c0, sm, zs0, zs1, part);
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);

@@ -575,8 +575,16 @@ class PDS2DStencilEngine(PDS2DEngine):
                     a.fkind, a.half, a.y = L.PCS_F_SEPCONV, half, self.y.data_ptr()
                     a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
                     a.cty = self.cty.data_ptr()
+                    # the N tables: backward / centred K take the fused normal-operator march (one
+                    # launch, pds_nmarch.hpp) when the library does -- supported with no gradient buffer
+                    self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+                    a.ntaps = self.ntaps.data_ptr()
+                    a.gbuf = None
+                    self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+                    a.gbuf = gsrc.data_ptr()
                     if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
-                        a.fkind, a.cty = fk, None
+                        a.fkind, a.cty, a.ntaps = fk, None, None
+                        self.nm_fused = False
                     else:
                         fk = self.fkind = L.PCS_F_SEPCONV
             if self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1:
@@ -615,11 +623,11 @@ class PDS2DStencilEngine(PDS2DEngine):
         self.bar = None
 
     def time_iteration_kernels(self, n):
-        """As PDS2DEngine's; the normal-operator march (separable PSF, SEPCONV here) is one
-        pcs_pds2d_step call holding two launches (N x into the gradient buffer, the step), timed as
-        'step' together and 'conv_nx' alone."""
+        """As PDS2DEngine's; with a separable PSF (SEPCONV here) either the fused normal-operator
+        march (one launch, `nm_fused`) or one pcs_pds2d_step call holding two launches (N x into the
+        gradient buffer, the step), timed as 'step' together and 'conv_nx' alone."""
         res = PDS2DEngine.time_iteration_kernels(self, n)
-        if self.fkind == L.PCS_F_SEPCONV:
+        if self.fkind == L.PCS_F_SEPCONV and not getattr(self, 'nm_fused', False):
             a, lib = self.args, self.lib
             ev = []
             for i in range(min(n, 50)):

@@ -391,11 +391,22 @@ class SlabPDS2D:
             # Conv^T y in fp64 on this rank's window only (own rows + the y halo), from the y rows
             # within the PSF's reach of it -- exact, since the sub-image's zero boundary falls where
             # the image's does or beyond the reach
-            if mode == 'sep':
+            if mode == 'sep' or (dtype == torch.float32 and half <= 7):
+                # 'sep_normal' too: backward / centred K run the fused normal-operator march when the
+                # library takes it (no N x pass, no gradient buffer read)
                 self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
                 a.ntaps = self.ntaps.data_ptr()
             self.cty = self._cty_window(spec, hy).to(dtype).contiguous()
             a.cty = self.cty.data_ptr()
+        self.nm_fused = False
+        if mode == 'sep_normal' and getattr(self, 'ntaps', None) is not None:
+            # supported without the gradient buffer = the fused march (the iterate pointers are bound
+            # per parity later: placeholders for the query, never written)
+            saved = (a.gbuf, a.x, a.xn, a.z, a.zn, a.partials)
+            ph = self.X[0].data_ptr()
+            a.gbuf, a.x, a.xn, a.z, a.zn, a.partials = None, ph, ph, ph, ph, ph
+            self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+            a.gbuf, a.x, a.xn, a.z, a.zn, a.partials = saved
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
         a.partials = self.partials.data_ptr()
@@ -417,7 +428,7 @@ class SlabPDS2D:
         self.native = bool(native)
         # the gradient passes of 'conv2d' / 'sep_normal' run once per iteration over the whole slab:
         # no banded (overlapped) schedule for them
-        self.overlap = bool(overlap) and mode in ('pointwise', 'sep')
+        self.overlap = bool(overlap) and (mode in ('pointwise', 'sep') or self.nm_fused)
         self._plan = None
         self._plan_key = None
         # multi-GPU native loop: chunks of 32 iterations replayed from a hipGraph (kernels, events

@@ -111,6 +111,30 @@ def test_slabs_general_k_and_conv_bitwise(name, world):
     assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
     assert torch.equal(z2, z1), (z2 - z1).abs().max().item()
     assert np.allclose(h2[1:], h1[1:], rtol=1e-5)
+    if name == 'sep_cen_f32':  # the fused normal-operator march (pds_nmarch.hpp GEN) on the slabs too
+        assert all(s.nm_fused for s in slabs)
+
+
+def test_slab_fused_normal_march_banded_bitwise():
+    """Separable PSF + centred K on the fused normal-operator march: the banded (boundary bands, then
+    interior) order on two slabs, bitwise the single-GPU engine."""
+    from pycsou_amd.parallel import SlabPDS2D, run_local
+    from tests.slab_worker import synth_problem
+    pds = synth_problem('sep_cen_f32')
+    pds.iterate()
+    eng = pds._engine
+    assert eng.nm_fused
+    n1 = pds.iter
+    x1, z1 = eng.X[n1 % 2].clone(), eng.Z[n1 % 2].clone()
+    pds2 = synth_problem('sep_cen_f32')
+    slabs = [SlabPDS2D.from_pds(pds2, None, rank=r, world=2) for r in range(2)]
+    assert all(s.nm_fused and s.overlap for s in slabs)
+    res = run_local(slabs, pds2.max_iter, pds2.min_iter, pds2.accuracy_threshold, split=True)
+    assert all(r[0] == n1 for r in res)
+    x2 = torch.cat([r[1] for r in res])
+    z2 = torch.cat([torch.cat([r[2].view(2, -1)[c] for r in res]) for c in range(2)])
+    assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
+    assert torch.equal(z2, z1), (z2 - z1).abs().max().item()
 
 
 def _c3(n0, n1, dtype):
@@ -172,7 +196,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize('name', ['deconv2d_l21_fwd_64_psf15', 'nonsep_cen_f32', 'cen_denoise_f32'])
+@pytest.mark.parametrize('name', ['deconv2d_l21_fwd_64_psf15', 'nonsep_cen_f32', 'cen_denoise_f32', 'sep_cen_f32'])
 def test_two_process_gloo(tmp_path, name):
     """Two ranks in two processes on the one GPU, gloo transport (host-staged): the golden
     separable deconvolution, a non-separable PSF with the reference's default centred K, and

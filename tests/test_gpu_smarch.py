@@ -130,7 +130,16 @@ CASES = [
     ((300, 200), 'lap', 'l1', 'sep4x6', '', True, (1.0, 1.0), (1.0, 1.0)),            # even lengths, partial strip
     ((261, 132), 'backward', 'l21', 'sep9', 'segment', True, (2.0, 0.5), (1, 1)),     # tier 7 half 4, 4-col strip
     ((130, 256), 'centered', 'l1', 'sep14x14', '', False, (1.0, 1.0), (1, 1)),        # even 14x14
+    # fused normal-operator march for backward / centred K (pds_nmarch.hpp GEN): one launch
+    ((200, 320), 'backward', 'l1', 'sep15', 'segment', True, (2.0, 0.5), (1, 1)),     # non-unit steps
+    ((96, 200), 'centered', 'l21', 'sep9', '', False, (1.0, 1.0), (1, 1)),            # 8-column last strip
+    ((150, 196), 'centered', 'l21', 'sep7', 'nonneg', True, (1.0, 1.0), (1, 1)),      # tier 3, 4-column strip
+    ((64, 4160), 'centered', 'l1', 'sep6x10', '', True, (1.0, 1.0), (1, 1)),         # 64 rows, even taps
 ]
+
+# (shape, K kind, PSF) -> the fused march must take it (last strip wider than the tier)
+FUSED = {('centered', 'sep15'), ('centered', 'sep14x14'), ('backward', 'sep15'), ('centered', 'sep9'),
+         ('centered', 'sep7'), ('centered', 'sep6x10')}
 
 
 @pytest.mark.parametrize('case', range(len(CASES)), ids=lambda i: f'{CASES[i][1]}-{CASES[i][0][0]}x{CASES[i][0][1]}')
@@ -145,6 +154,7 @@ def test_smarch_vs_oracle(case, monkeypatch):
     if fk.startswith('sep'):
         from pycsou_amd import _lib as L
         assert eng.fkind == L.PCS_F_SEPCONV and eng.cty is not None, 'separable PSF: normal-operator gradient'
+        assert eng.nm_fused == ((kind, fk) in FUSED), ('fused normal-operator march', kind, fk, eng.nm_fused)
     assert x.dtype == np.float32
     assert rel(x, xr) < 5e-5, rel(x, xr)
     assert rel(z, zr) < 5e-5, rel(z, zr)
@@ -165,3 +175,17 @@ def test_smarch_matches_tile_kernel(kind, monkeypatch):
     x0, z0, d0, e0 = _fused(p)
     assert e1.march and not e0.march
     assert rel(x1, x0) < 2e-6 and rel(z1, z0) < 2e-6
+
+
+@pytest.mark.parametrize('kind', ['centered', 'backward'])
+def test_fused_normal_march_matches_two_launch(kind, monkeypatch):
+    """Backward / centred K with a separable PSF: the fused normal-operator march (N x inside the
+    step) against the two-launch path (PCS_NMARCH_GEN=0: k_sep2d_nrm into a buffer + the stencil
+    march) on a 520 x 1024 problem -- the same iterates to fp32 rounding of two operation orders."""
+    args = ((520, 1024), kind, 'l21', 'sep15', 'nonneg', True, (1.0, 1.0), (1, 1))
+    p = _problem(*args, seed=11)
+    x1, z1, d1, e1 = _fused(p)
+    monkeypatch.setenv('PCS_NMARCH_GEN', '0')
+    x0, z0, d0, e0 = _fused(p)
+    assert e1.nm_fused and not e0.nm_fused
+    assert rel(x1, x0) < 2e-6 and rel(z1, z0) < 2e-6, (rel(x1, x0), rel(z1, z0))
