@@ -44,6 +44,11 @@ namespace pcs {
 #define PCS_SM_SAUX 16
 #endif
 
+// waves per SIMD the register budget targets (diagnostics builds override; 1 = no constraint)
+#ifndef PCS_SM_WPE
+#define PCS_SM_WPE 1
+#endif
+
 // wave priority 3 while a step's loads issue (as pds_pt.hpp); PCS_SM_PRIO=0 (diagnostics) drops it
 #ifndef PCS_SM_PRIO
 #define PCS_SM_PRIO 1
@@ -372,7 +377,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
 }
 
 template <int KK, int FK, int HK>
-__global__ __launch_bounds__(256) void k_pds2d_smarch(const float* __restrict__ x, float* __restrict__ xn,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE))) void k_pds2d_smarch(const float* __restrict__ x, float* __restrict__ xn,
                                                        const float* __restrict__ z, float* __restrict__ zn,
                                                        const float* __restrict__ gsrc,
                                                        const float* __restrict__ bsrc, Slab32 s, Params<float> P,
