@@ -359,8 +359,11 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
 // Tile rows: 16 for fp32 (vertical halo 2/16: PMC reads 1.39x -> ~1.24x the algorithmic at 8 rows;
 // 101 KB of LDS), 8 for fp64 (the 16-row rings would need 202 KB)
 constexpr int k3gTW = 128, k3gNT = 512;
+#ifndef PCS_3DG_ROWS32  // fp32 tile rows (diagnostics builds override)
+#define PCS_3DG_ROWS32 16
+#endif
 template <typename T>
-constexpr int k3g_rows() { return sizeof(T) == 4 ? 16 : 8; }
+constexpr int k3g_rows() { return sizeof(T) == 4 ? PCS_3DG_ROWS32 : 8; }
 
 template <typename T, int KK, int FK, bool VEC>
 __global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
