@@ -41,6 +41,11 @@
 #ifndef PCS_NM_EDGE
 #define PCS_NM_EDGE 1
 #endif
+// b (= Conv^T y) rows loaded a whole step ahead of their use (1) or at the top of the step that uses
+// them (0: only PH hides their latency)
+#ifndef PCS_NM_BAHEAD
+#define PCS_NM_BAHEAD 0
+#endif
 // cache-policy bits of the x' / z' stores (16 = sc1: written through, not left dirty in L2)
 // C2 2048^2: 31.4 against 32.3 us per iteration, C3 4096^2: 112.7 against 113.9 us (two alternating
 // reps each, profiles/r3_store_policy_ab.txt)
@@ -642,6 +647,16 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 
   // ================= march: step k covers t rows [a+2H+1, a+2H+17), u / x' rows [a+1, a+17), z' rows [a, a+16)
   const int nsteps = (s1 - s0 + TS - 1) / TS;
+#if PCS_NM_BAHEAD
+  G4<T> bvn;  // b of the next step's update rows
+  T b5n, bm1n = T(0);
+  {
+    const uint32_t rb = vb.row_off(s0 + 1 + ui);
+    bvn = bload4(vb.r, rb + co_u);
+    b5n = bload4(vb.r, rb + co_b5).v[0];
+    if constexpr (GEN) bm1n = bload4(vb.r, rb + co_bm1).v[3];
+  }
+#endif
   int ub = 0;  // (16 k) mod UR: row r = a + j sits in u ring slot (j + ub) mod UR
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
@@ -653,10 +668,22 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
 #endif
     load_z(a, 0);
+#if PCS_NM_BAHEAD
+    bv = bvn;
+    b5 = b5n;
+    bm1 = bm1n;
+    {
+      const uint32_t rb = vb.row_off(a + 1 + TS + ui);
+      bvn = bload4(vb.r, rb + co_u);
+      b5n = bload4(vb.r, rb + co_b5).v[0];
+      if constexpr (GEN) bm1n = bload4(vb.r, rb + co_bm1).v[3];
+    }
+#else
     const uint32_t rb = vb.row_off(a + 1 + ui);
     bv = bload4(vb.r, rb + co_u);
     b5 = bload4(vb.r, rb + co_b5).v[0];
     if constexpr (GEN) bm1 = bload4(vb.r, rb + co_bm1).v[3];
+#endif
     load_xn(xnx, a + 2 * H + 1 + TS);
 #if PCS_NM_PRIO
     __builtin_amdgcn_s_setprio(0);
