@@ -178,6 +178,12 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   const bool cown = cin;                            // stored by this workgroup
   // GEN: the strip's columns c0 - 1 .. c0 + 64 >= 2 samples inside the image (no column edge rules)
   const bool cint = c0 >= 4 && c0 + TW + 3 <= n1 - 3;
+  // GEN extra columns: lane l of wave wv works on output (row 4 wv + (eo & 3), column c0 - 1 (eo < 4) or
+  // c0 + 64), eo = l / 8, window taps l % 8 + 8 j; its b value is loaded with the step's b (bm1)
+  const int elane = tid & 63, eo = elane >> 3, esub = elane & 7, eur = 4 * wv + (eo & 3);
+  const bool eright = eo >= 4;
+  const int ecol = eright ? c0 + TW : c0 - 1, ets = eright ? TW : SLM1, eti = eright ? TW + 4 : 3;
+  const uint32_t co_bx = GEN ? col_off(ecol, n1) : kOOB;
   uint32_t co_xn[KXN];
   int rr_xn[KXN];
 #pragma unroll
@@ -463,34 +469,41 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       T* urow = U + slot * WU + 4 * ug;
       st4(urow, uo);
       bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
-      // the two extra columns in ONE branch of the lanes that hold them (group 0: c0 - 1, >= H inside
-      // the image or outside it; the last group: c0 + 64, < n1 - H or the image's last group), with
-      // per-lane column / slot / tile index: the wave runs the vertical 4H+1-tap pass once, not twice
-      if (!(PCS_NMG_ABL & 1) && (ug == 0 || ug == GG - 1)) {
-        const bool left = ug == 0;
-        const int col = left ? c0 - 1 : c0 + TW, ts = left ? SLM1 : TW, ti = left ? 3 : TW + 4;
-        const T* q0 = TR + M::tslot(lr - 2 * H) * WT + ts;
-        T tv[NQ];
+      // the two extra columns, cooperatively: the wave's 8 outputs (its 4 rows x columns c0 - 1 and
+      // c0 + 64) take 8 lanes each, lane `esub` summing window taps esub, esub + 8, .. (and edge term
+      // esub), a 3-step xor reduction, then all 8 lanes evaluate the update and lane 0 of the group
+      // stores u.  Column c0 - 1 is >= H inside the image or outside it, c0 + 64 is < n1 - H or the
+      // image's last group (no edge rows of N_h); every lane of the wave does useful work instead of
+      // 8 lanes issuing a 29-read serial pass
+      if (!(PCS_NMG_ABL & 1)) {
+        const int elr = a + 1 + eur, egr = s.row0 + elr;
+        const T* q0 = TR + M::tslot(elr - 2 * H) * WT + ets;  // the window is contiguous (mirror rows)
+        T part_g = T(0);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) tv[q] = q0[q * WT];  // plain reads: issued together, then the FMAs
-        T gx = T(0);
-#pragma unroll
-        for (int q4 = 0; q4 < (NQ + 3) / 4; ++q4) {
-          const G4<T> w = lds4(Wq + 4 * q4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (4 * q4 + e < NQ) gx += w.v[e] * tv[4 * q4 + e];
+        for (int j = 0; j < (NQ + 7) / 8; ++j) {
+          const int q = esub + 8 * j;
+          if (q < NQ) part_g += Wq[q] * q0[q * WT];
         }
-        if (vedge) {
-#pragma unroll
-          for (int k = 0; k < H; ++k) gx -= ((top || bot) ? d[k] : T(0)) * TR[(M::tslot(kr0) + k) * WT + ts];
+        if (vedge) {  // the exact rows of N_v near an image edge: term k = esub
+          const bool etop = egr >= 0 && egr < H, ebot = egr >= n0 - H && egr < n0;
+          const T* ed = Wq + 64 + (etop ? 8 * egr : 8 * H + 8 * (egr - (n0 - H)));
+          if (esub < H && (etop || ebot)) part_g -= ed[esub] * TR[(M::tslot(kr0) + esub) * WT + ets];
         }
-        const T xe = XR[(lr & 31) * WX + XL + (col - c0)];
-        const T w0[5] = {T(0), Z0[ui * WZ0 + ti], Z0[(ui + 1) * WZ0 + ti], Z0[(ui + 2) * WZ0 + ti], T(0)};
-        const T* z1e = Z1 + (ui + 1) * WZ1 + ti;
+        part_g += __shfl_xor(part_g, 1, 64);
+        part_g += __shfl_xor(part_g, 2, 64);
+        part_g += __shfl_xor(part_g, 4, 64);
+        const T xe = XR[(elr & 31) * WX + XL + (ecol - c0)];
+        const T w0[5] = {T(0), Z0[eur * WZ0 + eti], Z0[(eur + 1) * WZ0 + eti], Z0[(eur + 2) * WZ0 + eti], T(0)};
+        const T* z1e = Z1 + (eur + 1) * WZ1 + eti;
         const T w1[5] = {T(0), z1e[-1], z1e[0], z1e[1], T(0)};
-        const T xt = xt_of(std::false_type{}, gx - (left ? bm1 : b5), xe, w0, w1, col);
-        U[slot * WU + ts] = (rrow && (unsigned)col < (unsigned)n1) ? (T(2) * xt - xe) : T(0);
+        // K^T z on the extra column's row (egr) through xt_of's row index: recompute with egr
+        const T kt = pcs_fma(sw_d1_adj<KK, false>(w0, egr, n0, edge), P.inv_step0,
+                             sw_d1_adj<KK, false>(w1, ecol, n1, edge) * P.inv_step1);
+        const T xt = prox_g((xe - P.tau * (part_g - bm1)) - P.tau * kt, gk, P.seg_a, P.seg_b);
+        int eslot = eur + 1 + ub;
+        eslot = eslot >= UR ? eslot - UR : eslot;
+        const bool erow = (unsigned)egr < (unsigned)n0 && elr <= s.rows;
+        if (esub == 0) U[eslot * WU + ets] = (erow && (unsigned)ecol < (unsigned)n1) ? (T(2) * xt - xe) : T(0);
       }
     }
   };
@@ -600,10 +613,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 
   // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0 (GEN: t rows from s0 - 2H - 1,
   // u on rows s0 - 1 and s0)
-  // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5; GEN:
-  // group 0 also column c0 - 1, bm1)
+  // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5; GEN: the
+  // lane's extra-column output, bm1)
   const uint32_t co_b5 = ug == GG - 1 ? col_off(c0 + TW, n1) : kOOB;
-  const uint32_t co_bm1 = (GEN && ug == 0) ? col_off(c0 - 4, n1) : kOOB;
   constexpr int PR = GEN ? 1 : 0;  // extra prologue rows
   G4<T> xnx[KXN], bv;
   T b5, bm1 = T(0);
@@ -621,7 +633,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const uint32_t rbp = ui >= TS - 2 ? vb.row_off(s0 - TS + 1 + ui) : kOOB;
       bv = bload4(vb.r, rbp + co_u);
       b5 = bload4(vb.r, rbp + co_b5).v[0];
-      bm1 = bload4(vb.r, rbp + co_bm1).v[3];
+      bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 - TS + 1 + eur) + co_bx), 0, 0));
     } else {
       bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
       b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
@@ -654,7 +666,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     const uint32_t rb = vb.row_off(s0 + 1 + ui);
     bvn = bload4(vb.r, rb + co_u);
     b5n = bload4(vb.r, rb + co_b5).v[0];
-    if constexpr (GEN) bm1n = bload4(vb.r, rb + co_bm1).v[3];
+    if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 + 1 + eur) + co_bx), 0, 0));
   }
 #endif
   int ub = 0;  // (16 k) mod UR: row r = a + j sits in u ring slot (j + ub) mod UR
@@ -676,13 +688,13 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const uint32_t rb = vb.row_off(a + 1 + TS + ui);
       bvn = bload4(vb.r, rb + co_u);
       b5n = bload4(vb.r, rb + co_b5).v[0];
-      if constexpr (GEN) bm1n = bload4(vb.r, rb + co_bm1).v[3];
+      if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + TS + eur) + co_bx), 0, 0));
     }
 #else
     const uint32_t rb = vb.row_off(a + 1 + ui);
     bv = bload4(vb.r, rb + co_u);
     b5 = bload4(vb.r, rb + co_b5).v[0];
-    if constexpr (GEN) bm1 = bload4(vb.r, rb + co_bm1).v[3];
+    if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
 #endif
     load_xn(xnx, a + 2 * H + 1 + TS);
 #if PCS_NM_PRIO
