@@ -149,6 +149,65 @@ def test_pds2d_reduce_only_argument_checks():
     assert lib.pcs_pds2d_step_bands(ctypes.byref(a), 0, 8, 56, 64, None) == -1
 
 
+def test_pds3d_general_k_argument_checks():
+    """pcs_pds3d_* with backward / centred K: an unknown K kind is rejected, and a multi-plane slab
+    needs z halos of two planes (K^T z reads z one plane past u's planes on both sides); the host
+    checks run before anything is launched (fake device addresses are never dereferenced)."""
+    import ctypes
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    a = _lib.Pds3Args()
+    a.dtype, a.fkind, a.hkind, a.gkind = _lib.PCS_F32, _lib.PCS_F_NULL, _lib.PCS_H_L21, _lib.PCS_G_NULL
+    a.n0, a.n1, a.n2, a.plane0, a.planes = 64, 64, 64, 16, 32
+    a.sigma = a.step0 = a.step1 = a.step2 = 1.0
+    for f in ('x', 'xn', 'z', 'zn', 'partials'):
+        setattr(a, f, 0x10000)
+    a.halo_x = a.halo_z = 1
+    a.kkind = _lib.PCS_FORWARD
+    assert lib.pcs_pds3d_nblocks_bands(ctypes.byref(a), 0, 32, 32, 32) > 0
+    for kind in (_lib.PCS_BACKWARD, _lib.PCS_CENTERED):
+        a.kkind, a.halo_z = kind, 1
+        assert lib.pcs_pds3d_step(ctypes.byref(a), None) == -1
+        assert lib.pcs_pds3d_nblocks_bands(ctypes.byref(a), 0, 32, 32, 32) == -1
+        a.halo_z = 2
+        assert lib.pcs_pds3d_nblocks_bands(ctypes.byref(a), 0, 32, 32, 32) > 0
+    a.kkind = 7
+    assert lib.pcs_pds3d_step(ctypes.byref(a), None) == -1
+
+
+def test_pds2d_sepconv_general_k_dispatch():
+    """Separable-PSF PDS with backward / centred K: the fused normal-operator march (no G buffer)
+    covers the shape when the last 64-column strip is wider than the tap tier; otherwise the step
+    needs the caller's G buffer (two-launch form) and is unsupported without one. A multi-row slab
+    needs halos of 2 + 2*tier rows. Host-side queries only (fake device addresses)."""
+    import ctypes
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    a = _lib.PdsArgs()
+    a.dtype, a.fkind, a.hkind, a.gkind = _lib.PCS_F32, _lib.PCS_F_SEPCONV, _lib.PCS_H_L21, _lib.PCS_G_NULL
+    a.kkind = _lib.PCS_K_GRAD_CENTERED
+    a.half = 7
+    a.n0 = a.rows = 256
+    a.sigma = a.step0 = a.step1 = 1.0
+    a.w0 = a.w1 = 0.5
+    for f in ('x', 'xn', 'z', 'zn', 'y', 'partials', 'taps0', 'taps1', 'cty', 'ntaps'):
+        setattr(a, f, 0x10000)
+    a.gbuf = None
+    a.n1 = 4096                      # last strip 64 wide: fused march
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+    a.n1 = 4096 + 4                  # last strip 4 wide (<= tier 7): two-launch form, needs G
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0
+    a.gbuf = 0x40000
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+    a.n1, a.gbuf = 4096, None
+    a.row0, a.rows = 64, 128         # slab: halos must cover 2 + 2*tier rows of x and y
+    a.halo_x = a.halo_y = 15
+    a.halo_z = 4
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0
+    a.halo_x = a.halo_y = 16
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+
+
 @pytest.mark.parametrize('half', [7, 5, 3, 2])
 def test_nmarch_tables_equal_dense_normal_operator(half):
     """The normal-operator march kernel's tables (pycsou_amd.opt.engine.nmarch_taps) rebuild

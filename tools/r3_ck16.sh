@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for lib in default nmf4 default nmf4; do
+for lib in default nmf4 default nmf4; do  # nmf4: tools/build_var.sh nmf4 -DPCS_NMG_ABL=4
   if [ $lib = default ]; then unset PCS_LIB_PATH; else export PCS_LIB_PATH=pycsou_amd/lib/var/$lib/libpycsou_hip.so; fi
   timeout -k 10 300 python bench.py --steps 300 --warmup 30 --legs "" --volumes "" --no-cpu-baseline --lipschitz analytic > gpurun_out/r3_ck16_$lib.json 2>/dev/null || exit $?
   python3 -c "
