@@ -46,7 +46,7 @@ int pcs_abi_version(void);
 /* ---------------------------------------------------------------- operators */
 
 /* FirstDerivative along `axis` (pycsou/linop/diff.py:24-130 -> pylops.FirstDerivative):
- * out = D_axis x.  ndim in 1..3, dims[ndim], step = sampling. */
+ * out = D_axis x.  ndim in 1..32, dims[ndim], step = sampling. */
 int pcs_deriv1_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step,
                    int kind, int edge, hipStream_t stream);
 /* Adjoint of the above (pylops FirstDerivative.rmatvec). */
@@ -55,14 +55,14 @@ int pcs_deriv1_adj(int dtype, const void* y, void* out, int ndim, const int64_t*
 
 /* SecondDerivative along `axis` (pycsou/linop/diff.py:133-219 -> pylops.SecondDerivative):
  * out[i] = (x[i+1] - 2 x[i] + x[i-1]) / step^2 inside; ends 0, or the one-sided second-order
- * stencils with `edge`.  ndim in 1..3. */
+ * stencils with `edge`.  ndim in 1..32. */
 int pcs_deriv2_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step,
                    int edge, hipStream_t stream);
 int pcs_deriv2_adj(int dtype, const void* y, void* out, int ndim, const int64_t* dims, int axis, double step,
                    int edge, hipStream_t stream);
 
 /* Gradient (pycsou/linop/diff.py:777-882 -> pylops.Gradient = VStack of FirstDerivative):
- * out[k*N:(k+1)*N] = D_k x for k < ndim.  steps[ndim]. */
+ * out[k*N:(k+1)*N] = D_k x for k < ndim (1..32; one launch per axis beyond 3).  steps[ndim]. */
 int pcs_grad_fwd(int dtype, const void* x, void* out, int ndim, const int64_t* dims, const double* steps,
                  int kind, int edge, hipStream_t stream);
 /* Gradient.adjoint: out = sum_k D_k^T z_k (accumulated in axis order, pylops VStack.rmatvec). */
@@ -101,7 +101,7 @@ int pcs_conv2d_plan_pack(int dtype, const double* psf, int kh, int kw, int off0,
 int pcs_conv2d_planned(int dtype, const void* x, void* out, int64_t n0, int64_t n1, const void* plan, int tier,
                        const void* b, double beta, hipStream_t stream);
 
-/* Convolve1D along `axis` of a 1..3-D array (pycsou/linop/conv.py:20-164 -> pylops Convolve1D):
+/* Convolve1D along `axis` of a 1..32-D array (pycsou/linop/conv.py:20-164 -> pylops Convolve1D):
  * out[i] = sum_t h[t] x[i + (off - t) e_axis].  Adjoint = flipped taps, off' = k-1-off. */
 int pcs_conv1d(int dtype, const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps,
                int k, int off, hipStream_t stream);

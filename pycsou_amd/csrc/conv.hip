@@ -835,11 +835,15 @@ static int sep2d(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, 
 template <typename T>
 static int conv1d(const void* x, void* out, int ndim, const int64_t* dims, int axis, const void* taps, int k, int off,
                   hipStream_t st) {
-  if (!x || !out || !taps || !dims || ndim < 1 || ndim > 3 || axis < 0 || axis >= ndim || k < 1 || off < 0 ||
+  // any ndim: the axis is the middle one of (outer, dims[axis], sa)
+  if (!x || !out || !taps || !dims || ndim < 1 || ndim > 32 || axis < 0 || axis >= ndim || k < 1 || off < 0 ||
       off >= k)
     return PCS_EINVAL;
   int64_t N = 1, sa = 1, outer = 1;
-  for (int i = 0; i < ndim; ++i) N *= dims[i];
+  for (int i = 0; i < ndim; ++i) {
+    if (dims[i] < 1) return PCS_EINVAL;
+    N *= dims[i];
+  }
   for (int i = axis + 1; i < ndim; ++i) sa *= dims[i];
   for (int i = 0; i < axis; ++i) outer *= dims[i];
   constexpr int VN = V16<T>::N;

@@ -30,6 +30,22 @@ static bool make_geo(int ndim, const int64_t* dims, Geo3& g) {
   return true;
 }
 
+// One axis of an N-D C-order array as the middle axis of (outer, n_axis, inner): a derivative
+// along that axis sees only the sample's position on it, so any ndim maps onto the 3-D kernels
+// with axis index 1 (PyLops 1.x FirstDerivative / SecondDerivative take any ndim).
+static constexpr int kMaxDims = 32;
+static bool make_geo_axis(int ndim, const int64_t* dims, int axis, Geo3& g) {
+  if (ndim < 1 || ndim > kMaxDims || dims == nullptr || axis < 0 || axis >= ndim) return false;
+  int64_t outer = 1, inner = 1;
+  for (int i = 0; i < ndim; ++i) {
+    if (dims[i] < 1) return false;
+    if (i < axis) outer *= dims[i];
+    if (i > axis) inner *= dims[i];
+  }
+  const int64_t d3[3] = {outer, dims[axis], inner};
+  return make_geo(3, d3, g);
+}
+
 __device__ __forceinline__ int64_t coord(const Geo3& g, int64_t p, int a) { return (p / g.s[a]) % g.n[a]; }
 
 // D_a x / D_a^T y at p (stencil.hpp cores with the axis geometry of g)
@@ -54,6 +70,15 @@ template <typename T>
 __global__ void k_deriv1_adj(const T* __restrict__ y, T* __restrict__ out, Geo3 g, int a, T h, int kind, int edge) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x)
     out[p] = d1_adj_at(y, g, p, a, h, kind, edge);
+}
+
+// out += D_a^T y: one Gradient block of an N-D (ndim > 3) adjoint, accumulated in axis order as
+// k_grad_adj does (VStack rmatvec sums the blocks in order)
+template <typename T>
+__global__ void k_deriv1_adj_acc(const T* __restrict__ y, T* __restrict__ out, Geo3 g, int a, T h, int kind,
+                                 int edge) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < g.N; p += (int64_t)gridDim.x * blockDim.x)
+    out[p] = out[p] + d1_adj_at(y, g, p, a, h, kind, edge);
 }
 
 template <typename T>
@@ -107,20 +132,43 @@ template <typename T>
 static int deriv1(bool adj, const void* in, void* out, int ndim, const int64_t* dims, int axis, double step, int kind,
                   int edge, hipStream_t st) {
   Geo3 g;
-  if (!make_geo(ndim, dims, g) || axis < 0 || axis >= ndim || kind < 0 || kind > 2 || !in || !out)
-    return PCS_EINVAL;
-  const int a = 3 - ndim + axis;
+  if (!make_geo_axis(ndim, dims, axis, g) || kind < 0 || kind > 2 || !in || !out) return PCS_EINVAL;
   const unsigned grid = grid_for(g.N, 256);
   if (!adj)
-    k_deriv1_fwd<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, a, (T)step, kind, edge);
+    k_deriv1_fwd<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, 1, (T)step, kind, edge);
   else
-    k_deriv1_adj<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, a, (T)step, kind, edge);
+    k_deriv1_adj<T><<<grid, 256, 0, st>>>((const T*)in, (T*)out, g, 1, (T)step, kind, edge);
   return launch_status();
+}
+
+// Gradient of an array with more than 3 axes: one launch per axis block (forward: block k of the
+// stacked output; adjoint: the first block written, the others accumulated in axis order)
+template <typename T>
+static int grad_nd(bool adj, const T* in, T* out, int ndim, const int64_t* dims, const double* steps, int kind,
+                   int edge, hipStream_t st) {
+  Geo3 g;
+  for (int k = 0; k < ndim; ++k)
+    if (!make_geo_axis(ndim, dims, k, g)) return PCS_EINVAL;
+  const unsigned grid = grid_for(g.N, 256);
+  for (int k = 0; k < ndim; ++k) {
+    make_geo_axis(ndim, dims, k, g);
+    if (!adj)
+      k_deriv1_fwd<T><<<grid, 256, 0, st>>>(in, out + k * g.N, g, 1, (T)steps[k], kind, edge);
+    else if (k == 0)
+      k_deriv1_adj<T><<<grid, 256, 0, st>>>(in, out, g, 1, (T)steps[k], kind, edge);
+    else
+      k_deriv1_adj_acc<T><<<grid, 256, 0, st>>>(in + k * g.N, out, g, 1, (T)steps[k], kind, edge);
+    const int rc = launch_status();
+    if (rc != PCS_OK) return rc;
+  }
+  return PCS_OK;
 }
 
 template <typename T>
 static int grad(bool adj, const void* in, void* out, int ndim, const int64_t* dims, const double* steps, int kind,
                 int edge, hipStream_t st) {
+  if (ndim > 3 && kind >= 0 && kind <= 2 && in && out && steps)
+    return grad_nd<T>(adj, (const T*)in, (T*)out, ndim, dims, steps, kind, edge, st);
   Geo3 g;
   if (!make_geo(ndim, dims, g) || kind < 0 || kind > 2 || !in || !out || !steps) return PCS_EINVAL;
   const T h0 = (T)steps[0], h1 = ndim > 1 ? (T)steps[1] : T(1), h2 = ndim > 2 ? (T)steps[2] : T(1);
@@ -136,9 +184,8 @@ template <typename T>
 static int deriv2(bool adj, const void* in, void* out, int ndim, const int64_t* dims, int axis, double step, int edge,
                   hipStream_t st) {
   Geo3 g;
-  if (!make_geo(ndim, dims, g) || axis < 0 || axis >= ndim || !in || !out) return PCS_EINVAL;
-  k_deriv2<T><<<grid_for(g.N, 256), 256, 0, st>>>((const T*)in, (T*)out, g, 3 - ndim + axis, (T)(step * step), edge,
-                                                  adj ? 1 : 0);
+  if (!make_geo_axis(ndim, dims, axis, g) || !in || !out) return PCS_EINVAL;
+  k_deriv2<T><<<grid_for(g.N, 256), 256, 0, st>>>((const T*)in, (T*)out, g, 1, (T)(step * step), edge, adj ? 1 : 0);
   return launch_status();
 }
 

@@ -121,8 +121,8 @@ class Convolve1DOp(LinearOperator):
         dims = (size,) if reshape_dims is None else tuple(int(s) for s in reshape_dims)
         if int(np.prod(dims)) != size:
             raise ValueError('reshape_dims and size are not compatible')
-        if not 1 <= len(dims) <= 3:
-            raise NotImplementedError('Convolve1D supports 1-D to 3-D arrays')
+        if not 1 <= len(dims) <= 32:
+            raise NotImplementedError('Convolve1D supports 1-D to 32-D arrays')
         super().__init__(shape=(size, size), dtype=np.dtype(dtype), is_explicit=False, lipschitz_cst=np.inf)
         self.filter, self.dims, self.axis, self.method = h, dims, int(axis), method
         self.k = h.size

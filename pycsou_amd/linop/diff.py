@@ -40,8 +40,8 @@ class FirstDerivativeOp(_DiffOp):
         dims = (size,) if shape is None else tuple(int(s) for s in shape)
         if int(np.prod(dims)) != size:
             raise ValueError('shape and size are not compatible')
-        if not 1 <= len(dims) <= 3:
-            raise NotImplementedError('FirstDerivative supports 1-D to 3-D arrays')
+        if not 1 <= len(dims) <= 32:
+            raise NotImplementedError('FirstDerivative supports 1-D to 32-D arrays')
         super().__init__((size, size), size, dtype)
         self.dims, self.axis, self.step, self.edge, self.kind = dims, int(axis), float(step), bool(edge), kind
 
@@ -64,8 +64,8 @@ class GradientOp(_DiffOp):
         if kind not in ('forward', 'centered', 'backward'):
             raise NotImplementedError('kind must be forward, centered, or backward')
         dims = tuple(int(s) for s in shape)
-        if not 1 <= len(dims) <= 3:
-            raise NotImplementedError('Gradient supports 1-D to 3-D arrays')
+        if not 1 <= len(dims) <= 32:
+            raise NotImplementedError('Gradient supports 1-D to 32-D arrays')
         N = int(np.prod(dims))
         super().__init__((len(dims) * N, N), N, dtype)
         self.dims, self.steps, self.edge, self.kind = dims, _steps(step, len(dims)), bool(edge), kind
@@ -112,8 +112,8 @@ class SecondDerivativeOp(_DiffOp):
         dims = (size,) if shape is None else tuple(int(s) for s in shape)
         if int(np.prod(dims)) != size:
             raise ValueError('shape and size are not compatible')
-        if not 1 <= len(dims) <= 3:
-            raise NotImplementedError('SecondDerivative supports 1-D to 3-D arrays')
+        if not 1 <= len(dims) <= 32:
+            raise NotImplementedError('SecondDerivative supports 1-D to 32-D arrays')
         super().__init__((size, size), size, dtype)
         self.dims, self.axis, self.step, self.edge = dims, int(axis), float(step), bool(edge)
 

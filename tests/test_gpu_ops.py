@@ -35,7 +35,8 @@ def A():
 
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
-@pytest.mark.parametrize('shape', [(64, 64), (63, 65), (2, 17), (5, 6, 7), (16, 17, 18), (129,)])
+@pytest.mark.parametrize('shape', [(64, 64), (63, 65), (2, 17), (5, 6, 7), (16, 17, 18), (129,), (3, 4, 5, 6),
+                                   (2, 3, 3, 4, 5), (4, 3, 2, 3, 2, 3)])
 @pytest.mark.parametrize('kind', ['forward', 'backward', 'centered'])
 @pytest.mark.parametrize('edge', [True, False])
 def test_gradient(A, dtype, shape, kind, edge):
@@ -62,6 +63,29 @@ def test_first_derivative(A, dtype, axis):
     for kind in ['forward', 'backward', 'centered']:
         ref = P.FirstDerivative(990, dims=shape, dir=axis, sampling=0.5, edge=True, kind=kind)
         op = FirstDerivative(990, shape=shape, axis=axis, step=0.5, kind=kind)
+        assert rel(op(x), ref.matvec(x.astype(np.float64))) < TOL[dtype]
+        assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('axis', [0, 1, 2, 3])
+def test_derivatives_4d(A, dtype, axis):
+    """FirstDerivative / SecondDerivative of a 4-D array along each axis (PyLops 1.x takes any
+    ndim; the kernels see the axis as the middle one of (outer, n, inner))."""
+    from pycsou_amd.linop.diff import FirstDerivative, SecondDerivative
+    shape = (5, 6, 7, 8)
+    N = int(np.prod(shape))
+    rng = np.random.default_rng(4 + axis)
+    x = rng.standard_normal(N).astype(dtype)
+    for kind in ['forward', 'backward', 'centered']:
+        for edge in (True, False):
+            ref = P.FirstDerivative(N, dims=shape, dir=axis, sampling=0.5, edge=edge, kind=kind)
+            op = FirstDerivative(N, shape=shape, axis=axis, step=0.5, kind=kind, edge=edge)
+            assert rel(op(x), ref.matvec(x.astype(np.float64))) < TOL[dtype]
+            assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < TOL[dtype]
+    for edge in (True, False):
+        ref = P.SecondDerivative(N, dims=shape, dir=axis, sampling=1.5, edge=edge)
+        op = SecondDerivative(N, shape=shape, axis=axis, step=1.5, edge=edge)
         assert rel(op(x), ref.matvec(x.astype(np.float64))) < TOL[dtype]
         assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < TOL[dtype]
 
@@ -200,6 +224,24 @@ def test_convolve1d_axis(A, dtype, axis, k, dims):
     from pycsou_amd.linop.conv import Convolve1D
     N = int(np.prod(dims))
     rng = np.random.default_rng(4)
+    h = rng.standard_normal(k)
+    x = rng.standard_normal(N).astype(dtype)
+    ref = P.Convolve1D(N, h, offset=P.pycsou_offset(k), dims=dims, dir=axis)
+    op = Convolve1D(N, h, reshape_dims=dims, axis=axis)
+    assert rel(op(x), ref.matvec(x.astype(np.float64))) < 10 * TOL[dtype]
+    assert rel(op.adjoint(x), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('axis', [0, 1, 2, 3])
+@pytest.mark.parametrize('k', [5, 20])
+def test_convolve1d_4d(A, dtype, axis, k):
+    """Convolve1D along each axis of a 4-D array (16-B-aligned inner extent: the strided / LDS-row
+    kernels for k <= 15, the generic kernel for k = 20)."""
+    from pycsou_amd.linop.conv import Convolve1D
+    dims = (3, 5, 6, 8)
+    N = int(np.prod(dims))
+    rng = np.random.default_rng(40 + axis)
     h = rng.standard_normal(k)
     x = rng.standard_normal(N).astype(dtype)
     ref = P.Convolve1D(N, h, offset=P.pycsou_offset(k), dims=dims, dir=axis)
@@ -361,7 +403,10 @@ def test_abi_errors(A):
     lib = L.gpu()
     t = torch.zeros(16, device='cuda')
     assert lib.pcs_grad_fwd(7, L.ptr(t), L.ptr(t), 2, L.i64s([4, 4]), L.dbls([1, 1]), 0, 1, L.stream()) == -1
-    assert lib.pcs_grad_fwd(0, L.ptr(t), L.ptr(t), 4, L.i64s([1, 1, 4, 4]), L.dbls([1] * 4), 0, 1, L.stream()) == -1
+    # any ndim up to 32 (no launch for these: 33 axes, or an empty axis)
+    assert lib.pcs_grad_fwd(0, L.ptr(t), L.ptr(t), 33, L.i64s([1] * 33), L.dbls([1] * 33), 0, 1, L.stream()) == -1
+    assert lib.pcs_grad_fwd(0, L.ptr(t), L.ptr(t), 4, L.i64s([1, 0, 4, 4]), L.dbls([1] * 4), 0, 1, L.stream()) == -1
+    assert lib.pcs_deriv1_fwd(0, L.ptr(t), L.ptr(t), 4, L.i64s([1, 1, 4, 4]), 4, 1.0, 0, 1, L.stream()) == -1
     assert lib.pcs_conv2d(0, L.ptr(t), L.ptr(t), 4, 4, L.ptr(t), 3, 3, 3, 1, None, 0.0, L.stream()) == -1
     with pytest.raises(L.HipError):
         L.check(lib.pcs_prox_l1(0, None, L.ptr(t), 16, 1.0, L.stream()), 'pcs_prox_l1')

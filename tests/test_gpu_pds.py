@@ -216,6 +216,38 @@ def test_pds_fused_crop_vs_oracle_fp32_512():
     assert rel(est['dual_variable'], zr) < 5e-5
 
 
+@pytest.mark.parametrize('kind', ['centered', 'forward'])
+def test_pds_4d_gradient_generic_vs_oracle(kind):
+    """TV denoising of a 4-D array (volume x time) through the generic device path: a 4-axis
+    Gradient (one derivative launch per axis) with L21 over the 4 components, 30 iterations,
+    fp64 against the oracle (PyLops 1.x Gradient takes any ndim)."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    from oracle import pylops1 as P
+    shape = (6, 7, 8, 9)
+    N = int(np.prod(shape))
+    rng = np.random.default_rng(11)
+    y = np.repeat(rng.standard_normal((6, 7, 1, 1)), 72, axis=2).reshape(-1) + 0.1 * rng.standard_normal(N)
+    steps = [1.0, 0.5, 1.5, 2.0]
+    lip = np.sqrt(sum(4.0 / s ** 2 for s in steps))
+    tau, sigma = OR.pds_step_sizes(1.0, lip)[:2]
+    Kr = P.Gradient(shape, sampling=steps, edge=True, kind=kind)
+    hprox = OR.postcomp(lambda v, t: OR.prox_l21_pixel(v, t, 4), 0.1)
+    xr, zr, _ = OR.pds(lambda x: x - y, lambda v, t: v, Kr.matvec, Kr.rmatvec,
+                       lambda w, s: OR.fenchel_prox(hprox, w, s), tau, sigma, 0.9, np.zeros(N), np.zeros(4 * N),
+                       max_iter=29, min_iter=29, accuracy_threshold=0.0)
+    K = Gradient(shape, step=steps, kind=kind)
+    K.lipschitz_cst = K.diff_lipschitz_cst = lip
+    pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y), H=0.1 * L21Norm(dim=4 * N, groups=np.tile(np.arange(N), 4)),
+              K=K, x0=np.zeros(N), z0=np.zeros(4 * N), max_iter=29, min_iter=29, accuracy_threshold=0.0, verbose=None)
+    est, _, _ = pds.iterate()
+    assert pds.iter == 30
+    assert rel(est['primal_variable'], xr) < 1e-9
+    assert rel(est['dual_variable'], zr) < 1e-9
+
+
 FUSED_3D = [n for n in pds_case_names() if '3d' in n]
 
 

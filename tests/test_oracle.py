@@ -86,7 +86,7 @@ def _dot_test(op, n, m, rng, dtype=np.float64):
     assert abs(a - b) <= 1e-10 * max(abs(a), abs(b), 1.0)
 
 
-@pytest.mark.parametrize('shape', [(17,), (8, 9), (5, 6, 7)])
+@pytest.mark.parametrize('shape', [(17,), (8, 9), (5, 6, 7), (3, 4, 5, 6)])
 @pytest.mark.parametrize('kind', ['forward', 'backward', 'centered'])
 @pytest.mark.parametrize('edge', [True, False])
 def test_gradient_adjoint(shape, kind, edge):
