@@ -279,6 +279,7 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
            'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
            'iteration_frac_of_hbm_peak_per_gpu': round(alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
            'alg_bytes_per_iter': alg, 'halo_bytes_per_side_per_iter': halo,
+           'axis0_folded': bool(getattr(eng, 'fold', False)),  # axis-0 pass inside k_pds3d (13 words/voxel)
            'banded_overlap': bool(getattr(eng, 'banded', False) and eng.overlap),
            'banded_order': ((eng.order if eng.overlap else 'serial') if getattr(eng, 'banded', False) else None)
                            if world > 1 else None,

@@ -37,7 +37,7 @@ enum { PCS_H_L1 = 0, PCS_H_L21 = 1 };
 /* G functional kinds in the fused step */
 enum { PCS_G_NULL = 0, PCS_G_NONNEG = 1, PCS_G_SEGMENT = 2 };
 /* F kinds in the fused step */
-enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3, PCS_F_CONV2D = 4 };
+enum { PCS_F_NULL = 0, PCS_F_DENOISE = 1, PCS_F_SEPCONV = 2, PCS_F_GRADBUF = 3, PCS_F_CONV2D = 4, PCS_F_CONV0 = 5 };
 /* finite-difference K of the fused 2-D steps */
 enum { PCS_K_GRAD_FORWARD = 0, PCS_K_GRAD_BACKWARD = 1, PCS_K_GRAD_CENTERED = 2, PCS_K_LAPLACIAN = 3 };
 
@@ -423,6 +423,14 @@ typedef struct {
   void* ws;               /* with hist: pcs_pds3d_ws_bytes() bytes, zeroed once */
   int kkind;              /* PCS_FORWARD (0), PCS_BACKWARD or PCS_CENTERED: Gradient(kind) */
   int edge;               /* Gradient(edge=...): the centred kind's one-sided end samples */
+  /* fkind PCS_F_CONV0 (ABI 5; fp32, forward K): the axis-0 Convolve1D of a separable 3-D PSF inside
+   * the step, grad F = C0^T (C0 g - conv0_w) along axis 0 with `g` holding the in-plane normal
+   * operator C12^T C12 x and conv0_w = C12^T y (both with halo_g planes; halo_g >= conv0_k when
+   * planes < n0); conv0_taps: conv0_k <= 15 device taps, conv0_off the Convolve1D offset.  Replaces
+   * the pcs_conv0_residual_adjoint pass (pycsou/linop/conv.py:20-164 along axis 0). */
+  const void* conv0_w;
+  const void* conv0_taps;
+  int conv0_k, conv0_off;
 } pcs_pds3d_args;
 
 int64_t pcs_pds3d_nblocks(const pcs_pds3d_args* a);

@@ -20,7 +20,7 @@ PCS_H_L1, PCS_H_L21 = 0, 1
 PCS_K_GRAD_FORWARD, PCS_K_GRAD_BACKWARD, PCS_K_GRAD_CENTERED, PCS_K_LAPLACIAN = 0, 1, 2, 3
 PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
 PCS_APGD_G_L1 = 3
-PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF, PCS_F_CONV2D = 0, 1, 2, 3, 4
+PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF, PCS_F_CONV2D, PCS_F_CONV0 = 0, 1, 2, 3, 4, 5
 KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
 
 _c_int, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -62,7 +62,8 @@ class Pds3Args(ctypes.Structure):
                 ('tau', _c_dbl), ('sigma', _c_dbl), ('rho', _c_dbl), ('lam', _c_dbl),
                 ('step0', _c_dbl), ('step1', _c_dbl), ('step2', _c_dbl), ('seg_a', _c_dbl), ('seg_b', _c_dbl),
                 ('x', _vp), ('xn', _vp), ('z', _vp), ('zn', _vp), ('g', _vp),
-                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp), ('kkind', _c_int), ('edge', _c_int)]
+                ('partials', _vp), ('ctrl', _vp), ('hist', _vp), ('ws', _vp), ('kkind', _c_int), ('edge', _c_int),
+                ('conv0_w', _vp), ('conv0_taps', _vp), ('conv0_k', _c_int), ('conv0_off', _c_int)]
 
 
 class HaloSet(ctypes.Structure):

@@ -26,6 +26,7 @@
 #define PCS_3D_PRIO 0
 #endif
 
+
 namespace pcs {
 
 template <typename T>
@@ -130,13 +131,22 @@ __device__ __forceinline__ void gstore(T* p, const G4<T>& g, int c, int n2) {
 // (PMC: 1.53x the algorithmic reads); at 128 columns it is one line in five
 constexpr int k3T1 = 8, k3TW = PCS_K3TW, k3NT = PCS_K3TW == 64 ? 256 : PCS_K3TW == 128 ? 512 : 1024;
 
+// fkind PCS_F_CONV0: grad F = C0^T (C0 t - w) along axis 0 inside the update, t (the `g` array) the
+// in-plane normal operator C12^T C12 x and w = C12^T y: per U item two 15-plane register rings
+// (t, and the residual r = C0 t - w), the arithmetic of k_conv0_rta (conv.hip) sample for sample
+constexpr int k3C0K = 15;
+
 template <typename T, int FK, bool VEC>
-__global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
+__global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
                                                  const T* __restrict__ z, T* __restrict__ zn,
                                                  const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk,
                                                  double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
-                                                 int tiles1, int tiles2, Bands bd, int ntasks) {
-  constexpr int T1 = k3T1, TW = k3TW, NT = k3NT;
+                                                 int tiles1, int tiles2, Bands bd, int ntasks,
+                                                 const T* __restrict__ w0, const T* __restrict__ taps0, int k0,
+                                                 int off0) {
+  // PCS_F_CONV0: a second set of k3NT threads (waves 8-15) runs the axis-0 rings beside the update
+  constexpr bool FOLD = FK == PCS_F_CONV0;
+  constexpr int T1 = k3T1, TW = k3TW, NT = FOLD ? 2 * k3NT : k3NT;
   constexpr int UR = T1 + 1, WG = TW + 4, GG = WG / 4;
   constexpr int NU = UR * GG;                 // U items (x_t / u), 153
   constexpr int NZ = T1 * (TW / 4);           // z' items, 128
@@ -185,11 +195,84 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
                     ((c_z == v.n2 - 4) ? 64 : 0) | ((i1z == v.n1 - 1) ? 128 : 0);
 
   G4<T> xr, gr, z0r, z1r, z2r;
+  // ---- PCS_F_CONV0 ring waves: ring item = 3 consecutive voxels of the U tile (rows [r1, r1 + T1],
+  // cols [c2, c2 + WG)), two 15-plane register rings per voxel, tw[KR-1-j] = t(P - j) and
+  // rw[KR-1-j] = r(P - off0 - j), the taps zero-padded to 15 (g(P - 14) from the push of t(P));
+  // g(p + 1) lands in GS while the update waves work on plane p
+  constexpr int KR = FOLD ? k3C0K : 1, RV = 3;
+  constexpr int UWAVES = (NU + 63) / 64, NRI = UR * WG / RV;
+  static_assert(WG % RV == 0 && NRI <= k3NT, "ring items: whole rows, one per ring thread");
+  __shared__ __attribute__((aligned(16))) T GS[2][FOLD ? SZU : 4];
+  const bool ring_wave = FOLD && tid >= k3NT;  // wave-uniform
+  const bool u_wave = (tid >> 6) < UWAVES;
+  const int rr = tid - k3NT, ritem = min(max(rr, 0), NRI - 1);
+  const int rrow = (ritem * RV) / WG, rcol = ritem * RV - rrow * WG;
+  uint32_t roff[RV];
+#pragma unroll
+  for (int m = 0; m < RV; ++m) roff[m] = inplane<T>(v, r1 + rrow, c2 + rcol + m);
+  T h0[KR], tw[KR][RV], rw[KR][RV], tq[RV], wq[RV];
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+      h0[j] = j < k0 ? taps0[j] : T(0);
+#pragma unroll
+      for (int m = 0; m < RV; ++m) tw[j][m] = rw[j][m] = T(0);
+    }
+  }
+  auto load0 = [&](int Pl, T (&tv)[RV], T (&wv)[RV]) {  // t of plane Pl, w of plane Pl - off0
+    const Rsrc rt = plane_rsrc(g, v, v.hg, Pl), rw0 = plane_rsrc(w0, v, v.hg, Pl - off0);
+#pragma unroll
+    for (int m = 0; m < RV; ++m) {
+      tv[m] = bload1<T>(rt, roff[m]);
+      wv[m] = bload1<T>(rw0, roff[m]);
+    }
+  };
+  // push t(Pl): r(Pl - off0) = sum_j h0[j] t(Pl - j) - w (0 off the image / the stored planes);
+  // o = g(Pl - KR + 1) = sum_j h0[KR-1-j] r(Pl - off0 - j) (the adjoint's flipped taps): the sums
+  // of k_conv0_rta for 15 taps in its order
+  auto push0 = [&](int Pl, const T (&tv)[RV], const T (&wv)[RV], T (&o)[RV]) {
+#pragma unroll
+    for (int j = 0; j + 1 < KR; ++j)
+#pragma unroll
+      for (int m = 0; m < RV; ++m) tw[j][m] = tw[j + 1][m];
+#pragma unroll
+    for (int m = 0; m < RV; ++m) tw[KR - 1][m] = tv[m];
+    const int pr = Pl - off0, gpr = v.plane0 + pr;
+    const bool rv = gpr >= 0 && gpr < v.n0 && pr >= -v.hg && pr < v.planes + v.hg;
+    T acc[RV], sacc[RV];
+#pragma unroll
+    for (int m = 0; m < RV; ++m) acc[m] = sacc[m] = T(0);
+#pragma unroll
+    for (int j = 0; j < KR; ++j)
+#pragma unroll
+      for (int m = 0; m < RV; ++m) acc[m] += h0[j] * tw[KR - 1 - j][m];
+#pragma unroll
+    for (int j = 0; j + 1 < KR; ++j)
+#pragma unroll
+      for (int m = 0; m < RV; ++m) rw[j][m] = rw[j + 1][m];
+#pragma unroll
+    for (int m = 0; m < RV; ++m) {
+      const T rm = acc[m] - wv[m];
+      rw[KR - 1][m] = rv ? rm : T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < KR; ++j)
+#pragma unroll
+      for (int m = 0; m < RV; ++m) sacc[m] += h0[KR - 1 - j] * rw[KR - 1 - j][m];
+#pragma unroll
+    for (int m = 0; m < RV; ++m) o[m] = sacc[m];
+  };
+  auto gstore3 = [&](int slot, const T (&o)[RV]) {
+    if (rr < NRI) {
+#pragma unroll
+      for (int m = 0; m < RV; ++m) GS[slot][rrow * WG + rcol + m] = o[m];
+    }
+  };
   auto prefetch = [&](int p) {
     const Rsrc rx = plane_rsrc(x, v, v.hx, p), rz0 = plane_rsrc(z, v, v.hz, p),
                rz1 = plane_rsrc(z + zstride, v, v.hz, p), rz2 = plane_rsrc(z + 2 * zstride, v, v.hz, p);
     xr = gload<T, VEC>(rx, off_u);
-    if constexpr (FK != PCS_F_NULL) gr = gload<T, VEC>(plane_rsrc(g, v, v.hg, p), off_u);
+    if constexpr (FK != PCS_F_NULL && !FOLD) gr = gload<T, VEC>(plane_rsrc(g, v, v.hg, p), off_u);
     z0r = gload<T, VEC>(rz0, off_u);
     z1r = gload<T, VEC>(rz1, off_z1);
     z2r = gload<T, VEC>(rz2, off_z2);
@@ -201,6 +284,45 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
   };
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ring_wave) {  // the ring waves' own loop: the update loop's three barriers per plane
+    T o[RV];
+    {  // fill the rings up to t(p_start + KR - 1): g(p_start) -> GS
+      T tc[RV], wc[RV];
+      load0(p_start - KR + 1, tc, wc);
+      for (int Pl = p_start - KR + 1; Pl <= p_start + KR - 1; ++Pl) {
+        T tn[RV], wn[RV];
+        load0(Pl + 1, tn, wn);  // the last one is g(p_start + 1)'s t, kept in tq
+        push0(Pl, tc, wc, o);
+#pragma unroll
+        for (int m = 0; m < RV; ++m) {
+          tc[m] = tn[m];
+          wc[m] = wn[m];
+        }
+      }
+      gstore3(p_start & 1, o);
+#pragma unroll
+      for (int m = 0; m < RV; ++m) {
+        tq[m] = tc[m];
+        wq[m] = wc[m];
+      }
+    }
+    for (int p = p_start; p <= p_end; ++p) {
+      lds_barrier();
+      lds_barrier();
+      if (p < p_end) {  // g(p + 1) -> GS while the update waves work on plane p
+        T tc[RV], wc[RV];
+#pragma unroll
+        for (int m = 0; m < RV; ++m) {
+          tc[m] = tq[m];
+          wc[m] = wq[m];
+        }
+        load0(p + KR + 1, tq, wq);
+        push0(p + KR, tc, wc, o);
+        gstore3((p + 1) & 1, o);
+      }
+      lds_barrier();
+    }
+  } else {
   // prologue: z0 of plane p_start - 1 (for D0^T z0 at p_start), then plane p_start's data
   {
     const Rsrc rz0 = plane_rsrc(z, v, v.hz, p_start - 1);
@@ -214,7 +336,7 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
     lds_barrier();  // plane p-1's z' items are done with U[slot], Z*[slot]
     const G4<T> xv4 = xr;
     G4<T> gv4;
-    if constexpr (FK != PCS_F_NULL) gv4 = gr;
+    if constexpr (FK != PCS_F_NULL && !FOLD) gv4 = gr;
     land(slot);
 #if PCS_3D_PRIO
     __builtin_amdgcn_s_setprio(3);
@@ -226,7 +348,9 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
     lds_barrier();
     const int fl = launder(flags);
     // ---- U items: x_t, u on rows [r1, r1 + T1], cols [c2, c2 + WG) of plane p; x' on own cells
-    {  // every thread runs an item (surplus threads redo the last one; only real items store)
+    if (!FOLD || u_wave) {  // every thread runs an item (surplus threads redo the last one; only
+      // real items store); with FOLD the waves without real items skip it
+      if constexpr (FOLD) gv4 = lds4(&GS[slot][ui * WG + 4 * ug]);  // g(p)
       const G4<T> zb = lds4(&Z0[slot][ui * WG + 4 * ug]);         // z0(p)
       const G4<T> za = lds4(&Z0[prev][ui * WG + 4 * ug]);         // z0(p-1)
       const G4<T> z1a = lds4(&Z1[slot][ui * WG + 4 * ug]);        // z1(p, i1-1)
@@ -332,6 +456,7 @@ __global__ __launch_bounds__(k3NT) void k_pds3d(const T* __restrict__ x, T* __re
       }
     }
   }
+  }  // update waves
   block_sum<4>(part, red);
   if (hist != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
@@ -706,17 +831,20 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
   static_assert(k3gTW == k3TW, "the general-K kernel shares the forward kernel's column tiles");
-  if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
-    auto kern = a->kkind == PCS_BACKWARD ? k_pds3d_gen<T, PCS_BACKWARD, FK, VEC> : k_pds3d_gen<T, PCS_CENTERED, FK, VEC>;
-    kern<<<(unsigned)p.ntasks, k3gNT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g, v,
-                                               P, a->hkind, a->gkind, a->edge, a->partials, (Ctrl*)a->ctrl, a->hist,
-                                               a->ws, p.tiles1, p.tiles2, p.bd, p.ntasks);
-    return launch_status();
+  if constexpr (FK != PCS_F_CONV0) {
+    if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
+      auto kern =
+          a->kkind == PCS_BACKWARD ? k_pds3d_gen<T, PCS_BACKWARD, FK, VEC> : k_pds3d_gen<T, PCS_CENTERED, FK, VEC>;
+      kern<<<(unsigned)p.ntasks, k3gNT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g,
+                                                 v, P, a->hkind, a->gkind, a->edge, a->partials, (Ctrl*)a->ctrl,
+                                                 a->hist, a->ws, p.tiles1, p.tiles2, p.bd, p.ntasks);
+      return launch_status();
+    }
   }
-  k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, k3NT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn,
-                                                      (const T*)a->g, v, P, a->hkind, a->gkind, a->partials,
-                                                      (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.bd,
-                                                      p.ntasks);
+  k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, 0, st>>>(
+      (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g, v, P, a->hkind, a->gkind, a->partials,
+      (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.bd, p.ntasks, (const T*)a->conv0_w,
+      (const T*)a->conv0_taps, a->conv0_k, a->conv0_off);
   return launch_status();
 }
 
@@ -726,6 +854,9 @@ static int pds3d_v(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
     case PCS_F_NULL: return launch3<T, PCS_F_NULL, VEC>(a, pb, st);
     case PCS_F_DENOISE: return launch3<T, PCS_F_DENOISE, VEC>(a, pb, st);
     case PCS_F_GRADBUF: return launch3<T, PCS_F_GRADBUF, VEC>(a, pb, st);
+    case PCS_F_CONV0:
+      if constexpr (std::is_same<T, float>::value) return launch3<T, PCS_F_CONV0, VEC>(a, pb, st);
+      return PCS_EUNSUPPORTED;
     default: return PCS_EINVAL;
   }
 }
@@ -733,7 +864,7 @@ static int pds3d_v(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
 template <typename T>
 static int pds3d(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   const bool vec = a->n2 % 4 == 0 && aligned16_3(a->x) && aligned16_3(a->xn) && aligned16_3(a->z) &&
-                   aligned16_3(a->zn) && aligned16_3(a->g);
+                   aligned16_3(a->zn) && aligned16_3(a->g) && aligned16_3(a->conv0_w);
   return vec ? pds3d_v<T, true>(a, pb, st) : pds3d_v<T, false>(a, pb, st);
 }
 
@@ -771,6 +902,13 @@ static int check3(const pcs_pds3d_args* a) {
   if (a->n1 * a->n2 * esz > (1LL << 30) || a->n0 >= (1LL << 30)) return PCS_EUNSUPPORTED;  // one plane <= 1 GiB
   if (a->hist && (!a->ws || !a->ctrl || !aligned16_3(a->ws) || !aligned16_3(a->partials))) return PCS_EINVAL;
   if (a->dtype != PCS_F32 && a->dtype != PCS_F64) return PCS_EINVAL;
+  if (a->fkind == PCS_F_CONV0) {  // the axis-0 pass inside the forward-K update (fp32)
+    if (!a->g || !a->conv0_w || !a->conv0_taps || a->conv0_k < 1 || a->conv0_k > k3C0K || a->conv0_off < 0 ||
+        a->conv0_off >= a->conv0_k)
+      return PCS_EINVAL;
+    if (multi && a->halo_g < a->conv0_k) return PCS_EINVAL;  // t planes [-(k - 1), planes + k - 1]
+    if (a->kkind != PCS_FORWARD || a->dtype != PCS_F32) return PCS_EUNSUPPORTED;
+  }
   return PCS_OK;
 }
 

@@ -243,6 +243,24 @@ class PDS3DEngine:
         if self.ata:  # C12^T y on every stored plane (setup, once)
             self.yb = torch.empty_like(self.yw)
             self._sep_planes(L.ptr(self.yw), L.ptr(self.yb), self.rows + 2 * hg, self.inplane[::-1], True, L.stream())
+        # fp32 forward K: the axis-0 pass folded into the update (PCS_F_CONV0: g = C0^T (C0 t - C12^T y)
+        # from t = C12^T C12 x inside k_pds3d, whose second set of 512 threads keeps two 15-plane
+        # register rings per voxel): 13 words per voxel and iteration instead of 15, bitwise the same
+        # iterates; C4 1.63-1.65 ms against 1.72-1.74 ms with the separate pass
+        # (profiles/r3_ck30_fold_ab.txt).  PCS_3D_FOLD=0 keeps the separate pass.
+        self.fold = False
+        if self.ata and self.kkind == L.PCS_FORWARD and os.environ.get('PCS_3D_FOLD', '1') != '0':
+            _, h0, _, k0, off0 = self.ax0
+            b = L.Pds3Args()
+            ctypes.pointer(b)[0] = a
+            b.fkind, b.g, b.conv0_w, b.conv0_taps, b.conv0_k, b.conv0_off = (L.PCS_F_CONV0, self.T[0].data_ptr(),
+                                                                            self.yb.data_ptr(), h0.data_ptr(),
+                                                                            int(k0), int(off0))
+            b.x = b.xn = b.z = b.zn = self.X[0].data_ptr()  # placeholders: the query launches nothing
+            if int(self.lib.pcs_pds3d_nblocks_bands(ctypes.byref(b), 0, self.rows, self.rows, self.rows)) > 0:
+                a.fkind, a.g, a.conv0_w, a.conv0_taps, a.conv0_k, a.conv0_off = (b.fkind, b.g, b.conv0_w,
+                                                                                 b.conv0_taps, b.conv0_k, b.conv0_off)
+                self.fold = True
         self.args = [self._args_for(p) for p in (0, 1)]
         self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
@@ -345,8 +363,9 @@ class PDS3DEngine:
                          flipped, st)
 
     def _g_range(self, q0, q1, st):
-        """g = C^T (C x - y) on sub-volume planes [q0, q1) from the in-plane result in T0."""
-        if q1 <= q0:
+        """g = C^T (C x - y) on sub-volume planes [q0, q1) from the in-plane result in T0 (nothing
+        with the axis-0 pass folded into the update)."""
+        if q1 <= q0 or self.fold:
             return
         nsub = self.rows + 2 * self.hx
         img_lo, img_hi = self.hx - self.row0, self.hx - self.row0 + self.n0

@@ -434,6 +434,29 @@ def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
     assert rel(est['dual_variable'], z_ref) < tol
 
 
+@pytest.mark.parametrize('shape', [(24, 20, 24), (40, 24, 136), (17, 9, 132)])
+def test_pds3d_folded_axis0_bitwise(monkeypatch, shape):
+    """fp32 forward K: the axis-0 pass folded into k_pds3d (PCS_F_CONV0, register rings of t and
+    the residual) computes k_conv0_rta's sums in its order, so the iterates equal the separate
+    axis-0 pass (PCS_3D_FOLD=0) bit for bit; and they match the oracle."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    c = _vol_problem(0, np.float32, seed=9, niter=10, shape=shape)
+    out = []
+    for fold in ('1', '0'):
+        monkeypatch.setenv('PCS_3D_FOLD', fold)
+        pds = build(c, np.float32, engine='fused')
+        est, _, diag = pds.iterate()
+        assert isinstance(pds._engine, PDS3DEngine) and pds._engine.ata
+        assert pds._engine.fold == (fold == '1')
+        out.append((est['primal_variable'], est['dual_variable'],
+                    diag['Relative Improvement (primal variable)'].to_numpy(float)))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[0][2], out[1][2])
+    c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
+    x_ref, z_ref, _ = oracle_pds(c)
+    assert rel(out[0][0], x_ref) < 5e-5 and rel(out[0][1], z_ref) < 5e-5
+
+
 @pytest.mark.parametrize('shape,dtype,kind', [((20, 36, 260), np.float64, 'centered'), ((17, 9, 132), np.float32, 'centered'),
                                               ((12, 33, 130), np.float64, 'backward'), ((24, 20, 24), np.float32, 'backward')])
 def test_pds3d_general_k_vs_oracle(shape, dtype, kind):

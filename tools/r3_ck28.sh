@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 3 checkpoint 28: folded 3-D update with the rings on the U-item waves only; C4 A/B + kernel stats
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_pds.py -k "folded" \
+  > gpurun_out/r3_ck28_tests.txt 2>&1 || { tail -30 gpurun_out/r3_ck28_tests.txt; exit 1; }
+tail -1 gpurun_out/r3_ck28_tests.txt
+for f in 1 0 1; do
+  PCS_3D_FOLD=$f timeout -k 10 300 python bench.py --steps 20 --warmup 5 --legs "" --volumes c4:512:f32:20 --no-cpu-baseline --lipschitz analytic > gpurun_out/r3_ck28_fold$f.json 2>gpurun_out/r3_ck28_fold$f.err || { tail -20 gpurun_out/r3_ck28_fold$f.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/r3_ck28_fold$f.json').read().splitlines()[-1]); c=d['volume_c4']
+print('fold $f', c['it_per_s'], c['ms_per_iter'])"
+done
+PCS_3D_FOLD=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3_ck28_prof -o run -- python3 bench.py --steps 20 --warmup 5 --legs "" --volumes c4:512:f32:20 --no-cpu-baseline --lipschitz analytic > gpurun_out/r3_ck28_prof.log 2>&1 || { tail -20 gpurun_out/r3_ck28_prof.log; exit 1; }
+find gpurun_out/r3_ck28_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/r3_ck28_kernel_stats.csv
+python3 - <<'PY'
+import csv
+rows=list(csv.DictReader(open('gpurun_out/r3_ck28_kernel_stats.csv')))
+for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:8]:
+    print(r['Name'][:90], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')
+PY
