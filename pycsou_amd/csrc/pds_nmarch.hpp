@@ -94,6 +94,35 @@ __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// forward kernel: the strip's 65th column by 16 lanes per output (1) or by the last group's 4 lanes
+// per wave in a serial 29-read branch (0)
+#ifndef PCS_NM_COOP65
+#define PCS_NM_COOP65 1
+#endif
+
+// sum over the 16-lane DPP row holding the lane (every lane of the row gets the sum; the lanes of a
+// row add in different orders, so only one lane's value is used): row_ror 8, 4, 2, 1
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+  return v;
+}
+
+// forward kernel: PV / update / P6 in the column layout (1: a thread owns one column of the wave's four
+// rows -- b32 LDS reads, each t row of the window read once for four outputs, taps in VGPRs) or in the
+// row layout of PH (0: four columns of one row, every output row reading its own 29-row window)
+#ifndef PCS_NM_COLS
+#define PCS_NM_COLS 1
+#endif
+
+// 4-B store through a descriptor (kOOB offsets dropped), cache-policy bits AUX as bstore4
+template <int AUX = 0>
+__device__ __forceinline__ void bstore1(Rsrc r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, AUX);
+}
+
 // diagnostics builds (timing only, wrong results): 1 = GEN without its extra columns, 2 = GEN with
 // interior stencils everywhere, 4 = the forward kernel without its 65th column
 #ifndef PCS_NMG_ABL
@@ -111,7 +140,8 @@ struct NMarch {
   static constexpr int WX = TW + 2 * XL + 4;                       // x ring pitch (odd slot count)
   // t ring: 48 rows (a step's window + new rows: 4H + 2 TS <= 48 + TS) + a mirror of its first 4H
   // (rows 48..48+4H-1 repeat rows 0..4H-1), so any (4H+1)-row window starting in the ring is contiguous
-  static constexpr int XRING = 32, TRING = 48, TMIR = 4 * H;
+  // (forward, PCS_NM_COLS: 4H + 3, so the 4H + 4 rows of a wave's four-row window are contiguous too)
+  static constexpr int XRING = 32, TRING = 48, TMIR = GEN ? 4 * H : 4 * H + 3;
   static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B; GEN: 66)
   static constexpr int SLM1 = TW + 1;             // GEN: slot of column c0 - 1 in a t / u row
   // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 17 groups (from
@@ -184,6 +214,11 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   const bool eright = eo >= 4;
   const int ecol = eright ? c0 + TW : c0 - 1, ets = eright ? TW : SLM1, eti = eright ? TW + 4 : 3;
   const uint32_t co_bx = GEN ? col_off(ecol, n1) : kOOB;
+  // forward, PCS_NM_COOP65: lane l of wave wv works on the 65th column of row 4 wv + l / 16, window taps
+  // l % 16 + 16 j
+  const int fur = 4 * wv + (elane >> 4), fsub = elane & 15;
+  (void)fur;
+  (void)fsub;
   uint32_t co_xn[KXN];
   int rr_xn[KXN];
 #pragma unroll
@@ -406,6 +441,40 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       T* urow = U + slot * WU + 4 * ug;
       st4(urow, uo);
       bstore4<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_u, xo);
+#if PCS_NM_COOP65
+      // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0), cooperatively: the wave's 4
+      // outputs (its rows 4 wv + f, f = lane / 16) take 16 lanes each, lane fsub summing window taps
+      // fsub and fsub + 16 (and edge term fsub), a row_ror DPP reduction inside the 16-lane row, then
+      // every lane evaluates the update and lane fsub == 0 stores u (b65: the step's b at the column,
+      // loaded per lane with bv)
+      if (!(PCS_NMG_ABL & 4)) {
+        const int flr = a + 1 + fur, fgr = s.row0 + flr;
+        const T* q0 = TR + M::tslot(flr - 2 * H) * WT + TW;  // the window is contiguous (mirror rows)
+        T pg = T(0);
+#pragma unroll
+        for (int j = 0; j < (NQ + 15) / 16; ++j) {
+          const int q = fsub + 16 * j;
+          if (q < NQ) pg += Wq[q] * q0[q * WT];
+        }
+        if (vedge) {  // the exact rows of N_v near an image edge: term k = fsub
+          const bool ftop = fgr >= 0 && fgr < H, fbot = fgr >= n0 - H && fgr < n0;
+          const T* fd = Wq + 64 + (ftop ? 8 * fgr : 8 * H + 8 * (fgr - (n0 - H)));
+          if (fsub < H && (ftop || fbot)) pg -= fd[fsub] * TR[(M::tslot(kr0) + fsub) * WT + TW];
+        }
+        pg = row_sum16(pg);
+        const T xe = XR[(flr & 31) * WX + XL + TW];
+        const bool f_last = fgr >= n0 - 1, f_first = fgr <= 0;
+        T d0 = f_first ? T(0) : Z0[fur * WZ0 + TW];
+        if (!f_last) d0 -= Z0[(fur + 1) * WZ0 + TW];
+        const T d1 = Z1[(fur + 1) * WZ1 + TW + 3] - Z1[(fur + 1) * WZ1 + TW + 4];
+        const T xt = prox_g((xe - P.tau * (pg - b5)) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a,
+                            P.seg_b);
+        int fslot = fur + 1 + ub;
+        fslot = fslot >= UR ? fslot - UR : fslot;
+        const bool frow = fgr < n0 && flr <= s.rows;
+        if (fsub == 0) U[fslot * WU + TW] = (frow && c0 + TW < n1) ? (T(2) * xt - xe) : T(0);
+      }
+#else
       if (!(PCS_NMG_ABL & 4) && ug == GG - 1) {  // the strip's 65th column c0 + 64 (never the image's last: n1 % 4 == 0)
         const T* q0 = p0 + 4;
         T g4 = T(0);
@@ -425,6 +494,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
                            lds1(Z1 + (ui + 1) * WZ1 + TW + 4), false);
         urow[4] = (rrow && ucg + 4 < n1) ? (T(2) * xt - xe) : T(0);
       }
+#endif
     } else {  // backward / centred K: K^T z from z rows lr - 1 .. lr + 1, columns c - 1 .. c + 1
       const G4<T> xv4 = lds4(XR + (lr & 31) * WX + XL + 4 * ug);
       const T* z0p = Z0 + ui * WZ0 + 4 * ug + 4;  // tile row ui = row lr - 1, column c
@@ -611,11 +681,195 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     else p6f(a, ub);
   };
 
+  // ---- forward, PCS_NM_COLS: the column layout.  Lane `lane` of wave wv owns column cc = c0 + lane of
+  // the wave's rows: PV / update rows a + 1 + 4 wv + o, P6 rows a + 4 wv + o (o = 0..3).  PV reads the
+  // 4H + 4 window rows once each (b32, contiguous through the mirror) and feeds every row to the
+  // outputs it reaches; each output sums its taps in ascending order, as the row layout does
+  const int cc = c0 + lane;
+  const uint32_t co_cc = col_off(cc, n1);
+  const bool ccin = cc < n1, cclast = cc == n1 - 1;
+  T tv[NQ];  // N_v window taps (uniform, held in VGPRs: no LDS reads for them)
+  if constexpr (!GEN && PCS_NM_COLS) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tv[q] = to_vgpr(tq[q]);
+  }
+  auto pvc = [&](int a, const T (&bc)[4], T b5, int ub) {
+    const int lr0 = a + 1 + 4 * wv;
+    const T* p0 = TR + M::tslot(lr0 - 2 * H) * WT + lane;
+    constexpr int NR = NQ + 3, CH = 4, NCH = (NR + CH - 1) / CH;
+    T g[4] = {T(0), T(0), T(0), T(0)};
+    T buf[2][CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) buf[0][j] = lds1(p0 + j * WT);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+          if ((c + 1) * CH + j < NR) buf[(c + 1) & 1][j] = lds1(p0 + ((c + 1) * CH + j) * WT);
+      }
+      pcs_fence();
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int q = c * CH + j;
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int k = q - o;
+          if (q < NR && k >= 0 && k < NQ) g[o] += tv[k] * buf[c & 1][j];
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) pin1(g[o]);
+      pcs_fence();
+    }
+    const int wrow0 = s.row0 + lr0;  // the wave's first global row
+    const bool vedge = PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H);
+    const int kr0 = (wrow0 < H ? 0 : n0 - H) - s.row0;  // local row of the band's first image row
+    if (vedge) {  // exact rows of N_v near an image edge
+      T te[H];
+#pragma unroll
+      for (int k = 0; k < H; ++k) te[k] = lds1(TR + (M::tslot(kr0) + k) * WT + lane);  // contiguous (mirror)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const int gr = wrow0 + o;
+        const bool top = gr >= 0 && gr < H, bot = gr >= n0 - H && gr < n0;
+        const T* d = Wq + 64 + (top ? 8 * gr : bot ? 8 * H + 8 * (gr - (n0 - H)) : 0);
+#pragma unroll
+        for (int k = 0; k < H; ++k) g[o] -= ((top || bot) ? d[k] : T(0)) * te[k];
+      }
+    }
+    // update: z0 tile rows 4 wv .. 4 wv + 4 (row lr - 1 of output o at tile row 4 wv + o), z1 tile rows
+    // 4 wv + 1 + o at columns cc - 1 (index lane + 3) and cc (lane + 4)
+    T z0c[5];
+#pragma unroll
+    for (int o = 0; o < 5; ++o) z0c[o] = lds1(Z0 + (4 * wv + o) * WZ0 + lane);
+    T sdx = T(0), sx = T(0);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int lr = lr0 + o, gr = s.row0 + lr;
+      const T xv = lds1(XR + (lr & 31) * WX + XL + lane);
+      const T zl = lds1(Z1 + (4 * wv + 1 + o) * WZ1 + 3 + lane), zc = lds1(Z1 + (4 * wv + 1 + o) * WZ1 + 4 + lane);
+      const bool r_last = gr >= n0 - 1, r_first = gr <= 0;
+      const bool rrow = gr < n0 && lr <= s.rows;
+      const bool own = lr >= s0 && lr < s1 && gr < n0 && ccin;
+      T d0 = r_first ? T(0) : z0c[o];
+      if (!r_last) d0 -= z0c[o + 1];
+      const T d1 = zl - (cclast ? T(0) : zc);
+      const T xt = prox_g((xv - P.tau * (g[o] - bc[o])) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk,
+                          P.seg_a, P.seg_b);
+      int slot = 4 * wv + o + 1 + ub;
+      slot = slot >= UR ? slot - UR : slot;
+      U[slot * WU + lane] = (rrow && ccin) ? (T(2) * xt - xv) : T(0);
+      const T xnew = P.rho * xt + P.omr * xv;
+      bstore1<PCS_NM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_cc, xnew);
+      if (own) {
+        const T dx = xv - xnew;
+        sdx += dx * dx;
+        sx += xv * xv;
+      }
+    }
+    part[0] += (double)sdx;
+    part[1] += (double)sx;
+#if PCS_NM_COOP65
+    if (!(PCS_NMG_ABL & 4)) {  // the strip's 65th column, 16 lanes per output (as in pv)
+      const int flr = a + 1 + fur, fgr = s.row0 + flr;
+      const T* q0 = TR + M::tslot(flr - 2 * H) * WT + TW;
+      T pg = T(0);
+#pragma unroll
+      for (int j = 0; j < (NQ + 15) / 16; ++j) {
+        const int q = fsub + 16 * j;
+        if (q < NQ) pg += Wq[q] * q0[q * WT];
+      }
+      if (vedge) {
+        const bool ftop = fgr >= 0 && fgr < H, fbot = fgr >= n0 - H && fgr < n0;
+        const T* fd = Wq + 64 + (ftop ? 8 * fgr : fbot ? 8 * H + 8 * (fgr - (n0 - H)) : 0);
+        if (fsub < H && (ftop || fbot)) pg -= fd[fsub] * TR[(M::tslot(kr0) + fsub) * WT + TW];
+      }
+      pg = row_sum16(pg);
+      const T xe = XR[(flr & 31) * WX + XL + TW];
+      const bool f_last = fgr >= n0 - 1, f_first = fgr <= 0;
+      T d0 = f_first ? T(0) : Z0[fur * WZ0 + TW];
+      if (!f_last) d0 -= Z0[(fur + 1) * WZ0 + TW];
+      const T d1 = Z1[(fur + 1) * WZ1 + TW + 3] - Z1[(fur + 1) * WZ1 + TW + 4];
+      const T xt = prox_g((xe - P.tau * (pg - b5)) - P.tau * (d0 * P.inv_step0 + d1 * P.inv_step1), gk, P.seg_a,
+                          P.seg_b);
+      int fslot = fur + 1 + ub;
+      fslot = fslot >= UR ? fslot - UR : fslot;
+      const bool frow = fgr < n0 && flr <= s.rows;
+      if (fsub == 0) U[fslot * WU + TW] = (frow && c0 + TW < n1) ? (T(2) * xt - xe) : T(0);
+    }
+#else
+    static_assert(PCS_NM_COOP65 || !PCS_NM_COLS, "the column layout computes the 65th column cooperatively");
+#endif
+  };
+  // P6 in the column layout: z' on rows lr = a + 4 wv + o, column cc; u rows 4 wv + o .. 4 wv + 4 of the step
+  auto p6c = [&](int a, int ub) {
+    T uc[5];
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      int sl = 4 * wv + o + ub;
+      sl = sl >= 17 ? sl - 17 : sl;
+      uc[o] = lds1(U + sl * WU + lane);
+    }
+    T sdz = T(0), sz = T(0);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int lr = a + 4 * wv + o, gr = s.row0 + lr;
+      int sl = 4 * wv + o + ub;
+      sl = sl >= 17 ? sl - 17 : sl;
+      const T uright = lds1(U + sl * WU + lane + 1);
+      const T zv0 = lds1(Z0 + (4 * wv + o) * WZ0 + lane), zv1 = lds1(Z1 + (4 * wv + o) * WZ1 + 4 + lane);
+      const bool r_last = gr >= n0 - 1;
+      const bool own = lr >= s0 && lr < s1 && gr < n0 && ccin;
+      const T d0 = r_last ? T(0) : (uc[o + 1] - uc[o]);
+      const T d1 = cclast ? T(0) : (uright - uc[o]);
+      const T w0v = zv0 + P.sigma * (d0 * P.inv_step0), w1v = zv1 + P.sigma * (d1 * P.inv_step1);
+      T zt0, zt1;
+      if (HK == PCS_H_L21) {  // as p6f
+        const T sc = fminf(T(1), P.lam * fast_rsqrt(w0v * w0v + w1v * w1v));
+        zt0 = w0v * sc;
+        zt1 = w1v * sc;
+      } else {
+        zt0 = fminf(fmaxf(w0v, -P.lam), P.lam);
+        zt1 = fminf(fmaxf(w1v, -P.lam), P.lam);
+      }
+      const T o0 = P.rho * zt0 + P.omr * zv0, o1 = P.rho * zt1 + P.omr * zv1;
+      const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_cc;
+      bstore1<PCS_NM_SAUX>(rzn0, off, o0);
+      bstore1<PCS_NM_SAUX>(rzn1, off, o1);
+      if (own) {
+        const T e0 = zv0 - o0, e1 = zv1 - o1;
+        sdz += e0 * e0 + e1 * e1;
+        sz += zv0 * zv0 + zv1 * zv1;
+      }
+    }
+    part[2] += (double)sdz;
+    part[3] += (double)sz;
+  };
+  constexpr bool COLS = !GEN && PCS_NM_COLS;
+  static_assert(!COLS || !PCS_NM_BAHEAD, "the column layout loads b at the top of its step");
+  // b of the column layout: rows r0 + 4 wv + o, column cc
+  auto load_bc = [&](T (&bc)[4], int r0) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+      bc[o] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(r0 + 4 * wv + o) + co_cc), 0, 0));
+  };
+
   // ================= prologue: t rows [s0 - 2H, s0 + 2H], u / x' on row s0 (GEN: t rows from s0 - 2H - 1,
   // u on rows s0 - 1 and s0)
   // b of a group = its 4 columns (bv) and, for the last group, the strip's 65th column (b5; GEN: the
   // lane's extra-column output, bm1)
   const uint32_t co_b5 = ug == GG - 1 ? col_off(c0 + TW, n1) : kOOB;
+  // forward, PCS_NM_COOP65: every lane loads b of its 65th-column output (row r0 + fur), else the last
+  // group's lanes b of their own row's 65th column
+  const uint32_t co_f65 = col_off(c0 + TW, n1);
+  auto load_b5 = [&](int r0) -> T {
+    if constexpr (!GEN && PCS_NM_COOP65)
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(r0 + fur) + co_f65), 0, 0));
+    else
+      return bload4(vb.r, vb.row_off(r0 + ui) + co_b5).v[0];
+  };
   constexpr int PR = GEN ? 1 : 0;  // extra prologue rows
   G4<T> xnx[KXN], bv;
   T b5, bm1 = T(0);
@@ -636,7 +890,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 - TS + 1 + eur) + co_bx), 0, 0));
     } else {
       bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
-      b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
+      if constexpr (PCS_NM_COOP65) b5 = load_b5(s0 - TS + 1);  // row s0: wave 3's last output row
+      else b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
     }
 #pragma unroll
     for (int k = 0; k < KXP; ++k) {
@@ -665,7 +920,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   {
     const uint32_t rb = vb.row_off(s0 + 1 + ui);
     bvn = bload4(vb.r, rb + co_u);
-    b5n = bload4(vb.r, rb + co_b5).v[0];
+    b5n = load_b5(s0 + 1);
     if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 + 1 + eur) + co_bx), 0, 0));
   }
 #endif
@@ -687,13 +942,13 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     {
       const uint32_t rb = vb.row_off(a + 1 + TS + ui);
       bvn = bload4(vb.r, rb + co_u);
-      b5n = bload4(vb.r, rb + co_b5).v[0];
+      b5n = load_b5(a + 1 + TS);
       if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + TS + eur) + co_bx), 0, 0));
     }
 #else
     const uint32_t rb = vb.row_off(a + 1 + ui);
     bv = bload4(vb.r, rb + co_u);
-    b5 = bload4(vb.r, rb + co_b5).v[0];
+    b5 = load_b5(a + 1);
     if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
 #endif
     load_xn(xnx, a + 2 * H + 1 + TS);
