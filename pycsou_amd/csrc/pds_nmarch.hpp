@@ -112,15 +112,32 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 // forward kernel: PV / update / P6 in the column layout (1: a thread owns one column of the wave's four
 // rows -- b32 LDS reads, each t row of the window read once for four outputs, taps in VGPRs) or in the
-// row layout of PH (0: four columns of one row, every output row reading its own 29-row window)
+// row layout of PH (0: four columns of one row, every output row reading its own 29-row window).
+// Measured: parity green, but 123.8-125.0 against 107.1-111.0 us back to back (4 alternating reps,
+// profiles/r3_ck35_cols_ab.txt): the b32 stores / loads (12 + 4 VMEM instructions per thread and step
+// instead of 3 + 1) and the extra update reads cost more than the PV's halved LDS cycles save -- kept off
 #ifndef PCS_NM_COLS
-#define PCS_NM_COLS 1
+#define PCS_NM_COLS 0
 #endif
 
 // 4-B store through a descriptor (kOOB offsets dropped), cache-policy bits AUX as bstore4
 template <int AUX = 0>
 __device__ __forceinline__ void bstore1(Rsrc r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, AUX);
+}
+
+// GEN: the extra columns' 8-lane reduction by DPP (quad_perm xor 1, xor 2, row_half_mirror: VALU
+// latency) or by three ds_bpermute shuffles (0: LDS latency each); the same sums bit for bit
+#ifndef PCS_NMG_DPP
+#define PCS_NMG_DPP 1
+#endif
+// sum over the 8-lane group holding the lane (lanes 8 g .. 8 g + 7); every lane gets the same value, the
+// sums of __shfl_xor by 1, 2, 4 (fp addition commutes, and after the quad steps a quad holds one value)
+__device__ __forceinline__ float oct_sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));  // half mirror
+  return v;
 }
 
 // diagnostics builds (timing only, wrong results): 1 = GEN without its extra columns, 2 = GEN with
@@ -141,7 +158,7 @@ struct NMarch {
   // t ring: 48 rows (a step's window + new rows: 4H + 2 TS <= 48 + TS) + a mirror of its first 4H
   // (rows 48..48+4H-1 repeat rows 0..4H-1), so any (4H+1)-row window starting in the ring is contiguous
   // (forward, PCS_NM_COLS: 4H + 3, so the 4H + 4 rows of a wave's four-row window are contiguous too)
-  static constexpr int XRING = 32, TRING = 48, TMIR = GEN ? 4 * H : 4 * H + 3;
+  static constexpr int XRING = 32, TRING = 48, TMIR = (GEN || !PCS_NM_COLS) ? 4 * H : 4 * H + 3;
   static constexpr int WT = TW + 4, WU = TW + 4;  // t / u rows: 65 columns used (272 B; GEN: 66)
   static constexpr int SLM1 = TW + 1;             // GEN: slot of column c0 - 1 in a t / u row
   // z tiles (own __shared__ arrays, filled by LDS-DMA, lane-linear): z0 rows of 17 groups (from
@@ -559,9 +576,13 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
           const T* ed = Wq + 64 + (etop ? 8 * egr : 8 * H + 8 * (egr - (n0 - H)));
           if (esub < H && (etop || ebot)) part_g -= ed[esub] * TR[(M::tslot(kr0) + esub) * WT + ets];
         }
+#if PCS_NMG_DPP
+        part_g = oct_sum8(part_g);
+#else
         part_g += __shfl_xor(part_g, 1, 64);
         part_g += __shfl_xor(part_g, 2, 64);
         part_g += __shfl_xor(part_g, 4, 64);
+#endif
         const T xe = XR[(elr & 31) * WX + XL + (ecol - c0)];
         const T w0[5] = {T(0), Z0[eur * WZ0 + eti], Z0[(eur + 1) * WZ0 + eti], Z0[(eur + 2) * WZ0 + eti], T(0)};
         const T* z1e = Z1 + (eur + 1) * WZ1 + eti;
@@ -688,17 +709,15 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   const int cc = c0 + lane;
   const uint32_t co_cc = col_off(cc, n1);
   const bool ccin = cc < n1, cclast = cc == n1 - 1;
-  T tv[NQ];  // N_v window taps (uniform, held in VGPRs: no LDS reads for them)
-  if constexpr (!GEN && PCS_NM_COLS) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) tv[q] = to_vgpr(tq[q]);
-  }
   auto pvc = [&](int a, const T (&bc)[4], T b5, int ub) {
     const int lr0 = a + 1 + 4 * wv;
     const T* p0 = TR + M::tslot(lr0 - 2 * H) * WT + lane;
     constexpr int NR = NQ + 3, CH = 4, NCH = (NR + CH - 1) / CH;
+    static_assert(CH == 4, "chunk c's rows 4c .. 4c + 3 take taps of groups c - 1 and c");
     T g[4] = {T(0), T(0), T(0), T(0)};
     T buf[2][CH];
+    // taps 4 at a time (broadcast b128 reads, group c + 1 read one chunk ahead)
+    G4<T> wprev = {{T(0), T(0), T(0), T(0)}}, wcur = lds4(Wq), wnext;
 #pragma unroll
     for (int j = 0; j < CH; ++j) buf[0][j] = lds1(p0 + j * WT);
 #pragma unroll
@@ -707,6 +726,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #pragma unroll
         for (int j = 0; j < CH; ++j)
           if ((c + 1) * CH + j < NR) buf[(c + 1) & 1][j] = lds1(p0 + ((c + 1) * CH + j) * WT);
+        if (4 * (c + 1) < NQ) wnext = lds4(Wq + 4 * (c + 1));
       }
       pcs_fence();
 #pragma unroll
@@ -715,12 +735,17 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #pragma unroll
         for (int o = 0; o < 4; ++o) {
           const int k = q - o;
-          if (q < NR && k >= 0 && k < NQ) g[o] += tv[k] * buf[c & 1][j];
+          if (q < NR && k >= 0 && k < NQ) {
+            const T w = k >= 4 * c ? wcur.v[k - 4 * c] : wprev.v[k - 4 * (c - 1)];
+            g[o] += w * buf[c & 1][j];
+          }
         }
       }
 #pragma unroll
       for (int o = 0; o < 4; ++o) pin1(g[o]);
       pcs_fence();
+      wprev = wcur;
+      if (c + 1 < NCH && 4 * (c + 1) < NQ) wcur = wnext;
     }
     const int wrow0 = s.row0 + lr0;  // the wave's first global row
     const bool vedge = PCS_NM_EDGE && (wrow0 < H || wrow0 + 3 >= n0 - H);
@@ -873,6 +898,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   constexpr int PR = GEN ? 1 : 0;  // extra prologue rows
   G4<T> xnx[KXN], bv;
   T b5, bm1 = T(0);
+  T bc[4];  // COLS: b of the lane's column on the wave's four update rows
   {
     G4<T> xv[KXP];
 #pragma unroll
@@ -889,7 +915,8 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       b5 = bload4(vb.r, rbp + co_b5).v[0];
       bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 - TS + 1 + eur) + co_bx), 0, 0));
     } else {
-      bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
+      if constexpr (COLS) load_bc(bc, s0 - TS + 1);  // wave 3: rows s0 - 3 .. s0
+      else bv = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_u);
       if constexpr (PCS_NM_COOP65) b5 = load_b5(s0 - TS + 1);  // row s0: wave 3's last output row
       else b5 = bload4(vb.r, (ui == TS - 1 ? vb.row_off(s0) : kOOB) + co_b5).v[0];
     }
@@ -907,7 +934,10 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
   if (ui + TS < 4 * H + 1 + PR) ph(s0 - 2 * H - PR + TS + ui);  // t rows [.. + 16, s0 + 2H]
   lds_barrier();
   // u on row s0 (GEN: s0 - 1 too) -> the ring slots of step 0's rows a - 1, a; x' on row s0 (rows above: not own)
-  if (wv == 3) pv(s0 - TS, bv, b5, bm1, UR - TS);
+  if (wv == 3) {
+    if constexpr (COLS) pvc(s0 - TS, bc, b5, UR - TS);
+    else pv(s0 - TS, bv, b5, bm1, UR - TS);
+  }
   load_xn(xnx, s0 + 2 * H + 1);        // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
   lds_barrier();
   store_xn(xnx, s0 + 2 * H + 1);  // slots of rows [s0 + 2H - 31, s0 + 2H - 15): read by PH above only
@@ -946,8 +976,12 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + TS + eur) + co_bx), 0, 0));
     }
 #else
-    const uint32_t rb = vb.row_off(a + 1 + ui);
-    bv = bload4(vb.r, rb + co_u);
+    if constexpr (COLS) {
+      load_bc(bc, a + 1);
+    } else {
+      const uint32_t rb = vb.row_off(a + 1 + ui);
+      bv = bload4(vb.r, rb + co_u);
+    }
     b5 = load_b5(a + 1);
     if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
 #endif
@@ -956,11 +990,13 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     __builtin_amdgcn_s_setprio(0);
 #endif
     ph(a + 2 * H + 1 + ui);
-    vm_wait<KXN + 2 + PR>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
+    vm_wait<KXN + (COLS ? 5 : 2 + PR)>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
-    pv(a, bv, b5, bm1, ub);
+    if constexpr (COLS) pvc(a, bc, b5, ub);
+    else pv(a, bv, b5, bm1, ub);
     lds_barrier();
-    p6(a, ub);
+    if constexpr (COLS) p6c(a, ub);
+    else p6(a, ub);
     store_xn(xnx, a + 2 * H + 1 + TS);  // x ring slots of rows [a + 2H - 15, a + 2H + 1): read above
     if constexpr (GEN) ub = ub + TS >= UR ? ub + TS - UR : ub + TS;
     else ub = ub == 0 ? 16 : ub - 1;

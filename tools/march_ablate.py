@@ -24,7 +24,11 @@ def child():
     from pycsou_amd.opt.engine import PDS2DEngine
     torch.cuda.set_device(0)
     n = int(os.environ.get('PCS_N', '4096'))
-    pds = bench.build_problem(n, n, torch.float32)
+    pds = bench.build_problem(n, n, torch.float32, kind=os.environ.get('PCS_KIND', 'forward'))
+    if os.environ.get('PCS_KIND', 'forward') != 'forward':  # general-K engines: bench.py's timing
+        r = bench.fused_2d(pds, torch.float32, 200, 20)
+        print(f"RESULT {r['kernels_ms']['step'] * 1e3:.1f} {r['ms_per_step'] * 1e3:.1f} {r['nblocks']}", flush=True)
+        return
     spec = pds._fused_spec()
     eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, use_graph=False)
     N = 200
