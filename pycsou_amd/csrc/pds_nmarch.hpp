@@ -94,6 +94,17 @@ __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// cache-policy bits of the march's steady-state x / z / b loads (0: default; 2 = nt, streaming: measured
+// 113.6-115.9 against 109.9-112.2 us on C3, no change on the centred-K C3, profiles/r3_ck38_nt_*ab.txt)
+#ifndef PCS_NM_LAUX
+#define PCS_NM_LAUX 0
+#endif
+template <int AUX>
+__device__ __forceinline__ G4<float> bload4a(Rsrc r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
+  return {{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])}};
+}
+
 // forward kernel: the strip's 65th column by 16 lanes per output (1) or by the last group's 4 lanes
 // per wave in a serial 29-read branch (0)
 #ifndef PCS_NM_COOP65
@@ -247,7 +258,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 
   auto load_xn = [&](G4<T>(&xv)[KXN], int r0) {  // x rows [r0, r0 + TS) of the x region
 #pragma unroll
-    for (int k = 0; k < KXN; ++k) xv[k] = bload4(vx.r, vx.row_off(r0 + rr_xn[k]) + co_xn[k]);
+    for (int k = 0; k < KXN; ++k) xv[k] = bload4a<PCS_NM_LAUX>(vx.r, vx.row_off(r0 + rr_xn[k]) + co_xn[k]);
   };
   auto store_xn = [&](const G4<T>(&xv)[KXN], int r0) {
 #pragma unroll
@@ -276,9 +287,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
         const uint32_t o0 = (r0 >= ZR || r0 < rmin ? kOOB : vz0.row_off(a + r0)) + col_off(c0 - M::Z0C + 4 * g0, n1);
         const uint32_t o1 = (r1 >= ZR || r1 < rmin ? kOOB : vz1.row_off(a + r1)) + col_off(c0 - 4 + 4 * g1, n1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vz0.r, (__attribute__((address_space(3))) void*)(Z0 + 256 * j), 16,
-                                                 o0, 0, 0, 0);
+                                                 o0, 0, 0, PCS_NM_LAUX);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vz1.r, (__attribute__((address_space(3))) void*)(Z1 + 256 * j), 16,
-                                                 o1, 0, 0, 0);
+                                                 o1, 0, 0, PCS_NM_LAUX);
       }
     }
   };
@@ -980,7 +991,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       load_bc(bc, a + 1);
     } else {
       const uint32_t rb = vb.row_off(a + 1 + ui);
-      bv = bload4(vb.r, rb + co_u);
+      bv = bload4a<PCS_NM_LAUX>(vb.r, rb + co_u);
     }
     b5 = load_b5(a + 1);
     if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
