@@ -135,6 +135,17 @@ constexpr int k3T1 = 8, k3TW = PCS_K3TW, k3NT = PCS_K3TW == 64 ? 256 : PCS_K3TW 
 // in-plane normal operator C12^T C12 x and w = C12^T y: per U item two 15-plane register rings
 // (t, and the residual r = C0 t - w), the arithmetic of k_conv0_rta (conv.hip) sample for sample
 constexpr int k3C0K = 15;
+// PCS_F_CONV0 ring item width: 3 voxels per ring thread on waves 8-15, or 2 voxels on waves 6-15 (the
+// update loop's waves 6-7 have no items: U / z1 / z2 / z' items end in wave 5).  Measured C4 512^3:
+// 614-619 it/s at 3 against 562-570 at 2 (alternating, profiles/r3_ck39_ring_ab.txt)
+#ifndef PCS_3D_RV
+#define PCS_3D_RV 3
+#endif
+// planes of t / C12^T y in flight while the ring prologue fills the rings (loads issued that many
+// pushes ahead; 4 measured the same as 1, r3_ck39)
+#ifndef PCS_3D_RPD
+#define PCS_3D_RPD 1
+#endif
 
 template <typename T, int FK, bool VEC>
 __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
@@ -199,13 +210,17 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT) void k_pds3d(c
   // cols [c2, c2 + WG)), two 15-plane register rings per voxel, tw[KR-1-j] = t(P - j) and
   // rw[KR-1-j] = r(P - off0 - j), the taps zero-padded to 15 (g(P - 14) from the push of t(P));
   // g(p + 1) lands in GS while the update waves work on plane p
-  constexpr int KR = FOLD ? k3C0K : 1, RV = 3;
+  constexpr int KR = FOLD ? k3C0K : 1, RV = PCS_3D_RV;
   constexpr int UWAVES = (NU + 63) / 64, NRI = UR * WG / RV;
-  static_assert(WG % RV == 0 && NRI <= k3NT, "ring items: whole rows, one per ring thread");
+  // first ring thread: the update loop's item-free waves join the ring waves when RV = 2
+  constexpr int IWAVES = (cmax(cmax(NU, NZ), cmax(NZ1, NZ2)) + 63) / 64;  // waves holding update items
+  constexpr int RBASE = RV == 2 ? 64 * IWAVES : k3NT;
+  static_assert(!FOLD || (WG % RV == 0 && NRI <= NT - RBASE && RBASE <= k3NT && 64 * IWAVES <= RBASE),
+                "ring items: whole rows, one per ring thread, none on a wave with update items");
   __shared__ __attribute__((aligned(16))) T GS[2][FOLD ? SZU : 4];
-  const bool ring_wave = FOLD && tid >= k3NT;  // wave-uniform
+  const bool ring_wave = FOLD && tid >= RBASE;  // wave-uniform
   const bool u_wave = (tid >> 6) < UWAVES;
-  const int rr = tid - k3NT, ritem = min(max(rr, 0), NRI - 1);
+  const int rr = tid - RBASE, ritem = min(max(rr, 0), NRI - 1);
   const int rrow = (ritem * RV) / WG, rcol = ritem * RV - rrow * WG;
   uint32_t roff[RV];
 #pragma unroll
@@ -286,24 +301,34 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT) void k_pds3d(c
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   if (ring_wave) {  // the ring waves' own loop: the update loop's three barriers per plane
     T o[RV];
-    {  // fill the rings up to t(p_start + KR - 1): g(p_start) -> GS
-      T tc[RV], wc[RV];
-      load0(p_start - KR + 1, tc, wc);
-      for (int Pl = p_start - KR + 1; Pl <= p_start + KR - 1; ++Pl) {
-        T tn[RV], wn[RV];
-        load0(Pl + 1, tn, wn);  // the last one is g(p_start + 1)'s t, kept in tq
-        push0(Pl, tc, wc, o);
+    {  // fill the rings up to t(p_start + KR - 1): g(p_start) -> GS; the 2 KR - 1 pushes run in
+      // blocks of D with the loads of planes D ahead in flight (D register sets)
+      constexpr int D = PCS_3D_RPD, NP = 2 * KR - 1;
+      T tb[D][RV], wb[D][RV];
 #pragma unroll
-        for (int m = 0; m < RV; ++m) {
-          tc[m] = tn[m];
-          wc[m] = wn[m];
+      for (int j = 0; j < D; ++j) load0(p_start - KR + 1 + j, tb[j], wb[j]);
+      int Pl = p_start - KR + 1;
+      for (int i = 0; i < NP / D; ++i) {
+#pragma unroll
+        for (int j = 0; j < D; ++j, ++Pl) {
+          T tc[RV], wc[RV];
+#pragma unroll
+          for (int m = 0; m < RV; ++m) {
+            tc[m] = tb[j][m];
+            wc[m] = wb[j][m];
+          }
+          load0(Pl + D, tb[j], wb[j]);
+          push0(Pl, tc, wc, o);
         }
       }
+#pragma unroll
+      for (int j = 0; j < NP % D; ++j, ++Pl) push0(Pl, tb[j], wb[j], o);
+      // Pl = p_start + KR: its t / w sit in set NP % D (the last one issued for it)
       gstore3(p_start & 1, o);
 #pragma unroll
       for (int m = 0; m < RV; ++m) {
-        tq[m] = tc[m];
-        wq[m] = wc[m];
+        tq[m] = tb[NP % D][m];
+        wq[m] = wb[NP % D][m];
       }
     }
     for (int p = p_start; p <= p_end; ++p) {

@@ -41,6 +41,7 @@ struct RU4 {
   static constexpr int value = (V + 3) / 4 * 4;
 };
 constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <typename T>
 struct G4 {
