@@ -174,8 +174,13 @@ class HipError(ValueError):
     for invalid shapes/parameters; launch failures are reported the same way)."""
 
 
+# the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
+ABI_VERSION = 5
+
+
 def load():
-    """Load and declare the library (no GPU needed to load it)."""
+    """Load and declare the library (no GPU needed to load it).  A library built from other
+    sources than these declarations (a stale .so) is refused: its argument structs would not match."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -185,6 +190,9 @@ def load():
         for name, (res, args) in _SIGS.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
+        if lib.pcs_abi_version() != ABI_VERSION:
+            raise RuntimeError(f'pycsou_amd: {LIB_PATH} has ABI {lib.pcs_abi_version()}, these bindings expect '
+                               f'{ABI_VERSION} -- rebuild it with `make`')
         _lib = lib
     return _lib
 
