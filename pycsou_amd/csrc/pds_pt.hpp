@@ -67,7 +67,13 @@ __device__ __forceinline__ void pt_task(const float* __restrict__ x, float* __re
 
   const int ui = 2 * hb + lgrp, ug = lidx;  // P45 / P6: row ui of the step, column group ug
   const int ucg = c0 + 4 * ug;
-  const uint32_t co_u = col_off(ucg, n1), co_e = col_off(ucg + 4, n1);
+  // column c + 4 is kept by group 15 only: the other groups' fifth-column loads carry kOOB (no memory
+  // request; their fifth column is computed from zeros and dropped).  PCS_PT_E5=0: every group loads it
+#ifndef PCS_PT_E5
+#define PCS_PT_E5 1
+#endif
+  const uint32_t co_u = col_off(ucg, n1),
+                 co_e = (!PCS_PT_E5 || ug == TW / 4 - 1) ? col_off(ucg + 4, n1) : kOOB;
   uint32_t co_z0[KZ0], co_z1[KZ1];
   int rr_z0[KZ0], rr_z1[KZ1];
   // bit 2: U group in; 3: U column c + 4 in; 4: U group is the last

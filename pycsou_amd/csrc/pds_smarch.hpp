@@ -134,7 +134,12 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
   const int ce = ug == 0 ? c - 1 : c + 4;             // the item's fifth column
   const int lc = 4 + 4 * ug, lce = ug == 0 ? 3 : lc + 4;  // their ring columns
   const bool ext_st = ug == 0 || ug == TW / 4 - 1;   // fifth columns K u reads: c0 - 1, c0 + 64
-  const uint32_t co_c = col_off(c, n1), co_e = col_off(ce, n1);
+  // only groups 0 and 15 keep their fifth column: the others' fifth-column loads carry kOOB (no memory
+  // request; computed from zeros, never stored).  PCS_SM_E5=0: every group loads it
+#ifndef PCS_SM_E5
+#define PCS_SM_E5 1
+#endif
+  const uint32_t co_c = col_off(c, n1), co_e = (!PCS_SM_E5 || ext_st) ? col_off(ce, n1) : kOOB;
   // CI: the strip and its 4-column margins lie >= 2 columns inside the image (no column edge rule)
   const bool cin = CI || c < n1, ce_in = CI || (unsigned)ce < (unsigned)n1;
   uint32_t co_z[KZ];

@@ -179,9 +179,10 @@ class PDS3DEngine:
                 # 29-tap passes).  The axis-0 pass commutes with the in-plane ones, so
                 # g = C0^T (C0 (C12^T C12 x) - C12^T y) with C12^T y formed here once: two
                 # sub-volume passes per iteration instead of three (15 words/voxel, not 17).
-                # Default for fp32 (C4: 568-571 against 541-546 it/s); fp64 measured even (C5
-                # 36.2 it/s both ways: the in-plane work is FMA / LDS-bound, not HBM-bound), so
-                # it keeps the three-pass chain.  PCS_3D_ATA=0/1 overrides
+                # Default for fp32 (C4: 568-571 against 541-546 it/s); fp64 keeps the three-pass
+                # chain (C5 36.2 it/s both ways in round 2; 36.96-37.18 with the chain against
+                # 36.32-36.34 in round 3, profiles/r3_ck41_c5_ata_ab.txt: the in-plane work is
+                # FMA / LDS-bound, not HBM-bound).  PCS_3D_ATA=0/1 overrides
                 self.ata = False
                 ata_default = '1' if dtype == torch.float32 else '0'
                 if self.sep2 and os.environ.get('PCS_3D_ATA', ata_default) == '1':
