@@ -105,6 +105,13 @@ __device__ __forceinline__ G4<float> bload4a(Rsrc r, uint32_t off) {
   return {{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])}};
 }
 
+// step 0's x rows loaded with the prologue's own rows (1: one exposed load latency per segment instead of
+// two) or after the prologue's PV (0).  C3 106.7-106.9 against 107.0-107.8 us back to back, c3_cen
+// 135.7-136.0 against 138.0-138.1 (profiles/r3_ck43_xe_*ab.txt)
+#ifndef PCS_NM_XEARLY
+#define PCS_NM_XEARLY 1
+#endif
+
 // forward kernel: the strip's 65th column by 16 lanes per output (1) or by the last group's 4 lanes
 // per wave in a serial 29-read branch (0)
 #ifndef PCS_NM_COOP65
@@ -938,6 +945,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const int r = e / GXL, g = e - (e / GXL) * GXL;
       st4(XR + ((s0 - 2 * H - PR + r) & 31) * WX + 4 * g, xv[k]);
     }
+#if PCS_NM_XEARLY
+    load_xn(xnx, s0 + 2 * H + 1);  // step 0's x rows: in flight with the prologue's (parked after PH)
+#endif
     vm_wait<0>();
   }
   lds_barrier();
@@ -949,7 +959,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     if constexpr (COLS) pvc(s0 - TS, bc, b5, UR - TS);
     else pv(s0 - TS, bv, b5, bm1, UR - TS);
   }
+#if !PCS_NM_XEARLY
   load_xn(xnx, s0 + 2 * H + 1);        // step 0's x rows [s0 + 2H + 1, s0 + 2H + 17)
+#endif
   lds_barrier();
   store_xn(xnx, s0 + 2 * H + 1);  // slots of rows [s0 + 2H - 31, s0 + 2H - 15): read by PH above only
 
