@@ -44,6 +44,12 @@ namespace pcs {
 #define PCS_SM_SAUX 16
 #endif
 
+// step 0's z rows loaded and landed with the prologue's (1) or at step 0's top (0).  Parity green both
+// ways; no measurable difference on the 2048^2 legs (profiles/r3_ck44_ze_ab.txt): kept at 0
+#ifndef PCS_SM_ZEARLY
+#define PCS_SM_ZEARLY 0
+#endif
+
 // waves per SIMD the register budget targets (diagnostics builds override; 1 = no constraint)
 #ifndef PCS_SM_WPE
 #define PCS_SM_WPE 1
@@ -154,25 +160,30 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
   // x, y|g (and b) of the U items in two register sets: the set of step k + 1 loads at the top of
   // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index)
   G4<T> zr[D][KZ], xr[2], gr[2], br[2];
+#if PCS_SM_ZEARLY
+  G4<T> zr0[D][KZ];  // step 0's z rows, loaded with the prologue's (landed before the prologue's U)
+#endif
   T xe[2] = {T(0), T(0)}, ge[2] = {T(0), T(0)}, be[2] = {T(0), T(0)};
   // z rows [a + ZHI - 15, a + ZHI] (rows below rmin read as 0)
-  auto loads_z = [&](int a, int rmin) {
+  auto loads_z_into = [&](G4<T>(&dst)[D][KZ], int a, int rmin) {
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
       for (int k = 0; k < KZ; ++k) {
         const int r = a + M::ZHI - 15 + rr_z[k];
-        zr[d][k] = bload4(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
+        dst[d][k] = bload4(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
       }
   };
-  auto land_z = [&](int a) {
+  auto land_z_from = [&](const G4<T>(&src)[D][KZ], int a) {
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
       for (int k = 0; k < KZ; ++k)
         if (PCS_WAVE_ON(k, M::NZN))
-          st4(ZR + d * RING * WZ + ((a + M::ZHI - 15 + rr_z[k]) & 31) * WZ + lo_z[k], zr[d][k]);
+          st4(ZR + d * RING * WZ + ((a + M::ZHI - 15 + rr_z[k]) & 31) * WZ + lo_z[k], src[d][k]);
   };
+  auto loads_z = [&](int a, int rmin) { loads_z_into(zr, a, rmin); };
+  auto land_z = [&](int a) { land_z_from(zr, a); };
   // x and y|g of U row a + 1 + ui: the group and the fifth column
   auto loads_x = [&](auto pb, int a, int rmin) {
     constexpr int PB = decltype(pb)::value;
@@ -342,6 +353,20 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
   const int nsteps = (s1 - s0 + TS - 1) / TS;
+#if PCS_SM_ZEARLY
+  // step 0's z rows [s0 + ZHI - 15, s0 + ZHI] and the prologue's [s0 + ZHI - 31, s0 + ZHI - 16] fill the
+  // 32-row ring exactly: both load here and land before the prologue's U (one exposed load latency
+  // instead of two); the prologue's own U rows read no row of step 0's set
+  static_assert(M::ZHI - 15 > (KK == SK_LAP ? 2 : KK == PCS_FORWARD ? 0 : 1),
+                "the prologue's own U rows (<= s0) read no z row of step 0's set");
+  if (nsteps > 0) loads_z_into(zr0, s0, -(1 << 30));
+  loads_z(s0 - TS, s0 - M::ZPRO);
+  loads_x(P0{}, s0 - TS, s0 - M::UPRO);
+  if (nsteps > 0) loads_x(P1{}, s0, -(1 << 30));
+  lds_barrier();  // rings zeroed
+  land_z(s0 - TS);
+  if (nsteps > 0) land_z_from(zr0, s0);
+#else
   loads_z(s0 - TS, s0 - M::ZPRO);
   loads_x(P0{}, s0 - TS, s0 - M::UPRO);
   lds_barrier();  // rings zeroed
@@ -350,6 +375,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     loads_z(s0, -(1 << 30));
     loads_x(P1{}, s0, -(1 << 30));
   }
+#endif
   lds_barrier();
   uphase(std::false_type{}, P0{}, s0 - TS);
   // step k reads register set PB = (k + 1) & 1 and loads the other one for step k + 1
@@ -359,7 +385,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     // rows [a, a + 16] at >= 2 rows from both image edges (uniform)
     const bool ri = s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0;
     lds_barrier();  // the previous step's Z phase is done with the rings
-    land_z(a);
+    if (!PCS_SM_ZEARLY || k > 0) land_z(a);
     if (PCS_SM_PRIO) __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
     if (k + 1 < nsteps) {
       loads_z(a + TS, -(1 << 30));
