@@ -599,14 +599,21 @@ def slab_bench(n, dtype, K, W, world):
     pds = build_problem(n * world, n, dtype, lipschitz='analytic')
     comm = DistComm() if world > 1 else None
     kw = dict(rank=0 if comm is None else None, world=1 if comm is None else None)
-    try:  # the native loop (RCCL bound by the library) unless it cannot be set up on this box
-        eng = SlabPDS2D.from_pds(pds, comm, native=True, **kw)
-        eng.overlapped()
-    except Exception as e:  # noqa: BLE001 -- the torch.distributed-issued loop runs the same kernels
-        # reported in the line (top-level 'loop' / 'loop_fallback'), never silent
-        print(f'bench: WARNING native slab loop unavailable ({type(e).__name__}: {e}); falling back to the '
-              f'torch.distributed per-iteration loop (reported as loop_fallback=true)', file=sys.stderr)
+    fallback = False
+    if world > 1 and dist.get_backend() != 'nccl':
+        # gloo rehearsal (several ranks on one GPU): the library's RCCL binding needs one GPU per
+        # rank, so the torch.distributed-issued loop is the designed path here, not a fallback
         eng = SlabPDS2D.from_pds(pds, comm, native=False, **kw)
+    else:
+        try:  # the native loop (RCCL bound by the library) unless it cannot be set up on this box
+            eng = SlabPDS2D.from_pds(pds, comm, native=True, **kw)
+            eng.overlapped()
+        except Exception as e:  # noqa: BLE001 -- the torch.distributed-issued loop runs the same kernels
+            # reported in the line (top-level 'loop' / 'loop_fallback'), never silent
+            print(f'bench: WARNING native slab loop unavailable ({type(e).__name__}: {e}); falling back to the '
+                  f'torch.distributed per-iteration loop (reported as loop_fallback=true)', file=sys.stderr)
+            eng = SlabPDS2D.from_pds(pds, comm, native=False, **kw)
+            fallback = True
     del pds
     torch.cuda.empty_cache()
     total = W + K + 4
@@ -636,9 +643,96 @@ def slab_bench(n, dtype, K, W, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
-    loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else 'python'
+    loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else (
+        'python (gloo rehearsal)' if world > 1 and dist.get_backend() != 'nccl' else 'python')
     return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks,
-            'loop': loop, 'schedule_trial_ms': getattr(eng, 'tune_ms', None)}
+            'loop': loop, 'loop_fallback': fallback, 'schedule_trial_ms': getattr(eng, 'tune_ms', None)}
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, backend):
+    """`python bench.py --gpus N` without an external launcher: start N ranks as
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` in a child
+    process (never exec: nothing has touched the GPU yet, and the parent only waits) and return
+    its exit status.  With backend nccl the node must show N GPUs (device_count() does not
+    initialise the runtime)."""
+    n = args.gpus
+    if backend == 'nccl' and not args.launch_check:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f'bench: --gpus {n} needs {n} visible GPUs with backend nccl (one rank per GPU); '
+                  f'this node shows {have}.  Use PCS_BENCH_BACKEND=gloo for a one-GPU rehearsal.', file=sys.stderr)
+            return 2
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '1')
+    import subprocess
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args, world, backend):
+    """The rank count must be what --gpus asks for; nccl needs one GPU per local rank."""
+    if world != args.gpus:
+        print(f'bench: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree', file=sys.stderr)
+        sys.exit(2)
+    if backend == 'nccl' and world > 1 and not args.launch_check:
+        lw = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+        have = torch.cuda.device_count()
+        if have < lw:
+            print(f'bench: {lw} local ranks but {have} visible GPUs (backend nccl: one rank per GPU)', file=sys.stderr)
+            sys.exit(2)
+
+
+def launch_check(args, world, rank, backend):
+    """--launch-check: the launch path without GPU work -- join the process group, all-reduce the
+    rank ids, rank 0 prints the launch facts as one JSON line."""
+    if world > 1:
+        dev = 'cpu'
+        if backend == 'nccl':
+            dev = torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0')))
+            torch.cuda.set_device(dev)
+        dist.init_process_group(backend)
+        t = torch.tensor([float(rank)], device=dev)
+        dist.all_reduce(t)
+        ok = int(t.item()) == world * (world - 1) // 2
+        dist.destroy_process_group()
+    else:
+        ok = True
+    if rank == 0:
+        print(json.dumps({'launch_check': bool(ok), 'n_gpus': world, 'backend': backend,
+                          'parallelism': f'slab{world}' if world > 1 else 'single',
+                          'self_launched': os.environ.get('TORCHELASTIC_RUN_ID') is not None}), flush=True)
+    return 0 if ok else 1
+
+
+def headline_watchdog(args, rank, world, dtype):
+    """Watchdog on the N > 1 slab headline (the first multi-rank RCCL run): after
+    --headline-timeout seconds rank 0 prints the line with an `error` field and every rank exits
+    1, so a hang still yields a line and a non-zero status."""
+    def fire():
+        if rank == 0:
+            print(json.dumps({'metric': METRIC, 'value': None, 'unit': 'it/s', 'n_gpus': world,
+                              'steps': args.steps, 'warmup': args.warmup, 'higher_is_better': True,
+                              'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic',
+                              'config': {'workload': f'C3 TV-deconvolution {args.size}x{args.size} per GPU, slab engine',
+                                         'parallelism': f'slab{world}'},
+                              'error': f'slab headline: no result within {args.headline_timeout:.0f} s'}), flush=True)
+        sys.stderr.write(f'bench: rank {rank}: slab headline timed out\n')
+        sys.stderr.flush()
+        os._exit(1)
+    timer = threading.Timer(args.headline_timeout, fire)
+    timer.daemon = True
+    timer.start()
+    return timer
 
 
 def main():
@@ -661,14 +755,25 @@ def main():
                     help='operator norms of the single-GPU 2-D problems: compute_lipschitz_cst() or closed forms')
     ap.add_argument('--engine', default='auto', choices=['auto', 'slab'],
                     help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
+    ap.add_argument('--headline-timeout', type=float, default=420.0,
+                    help='watchdog (s) on the N > 1 slab headline: a stall prints the line with an error and exits 1')
+    ap.add_argument('--launch-check', action='store_true',
+                    help='start the ranks, join the process group, all-reduce once and print the launch facts '
+                         '(no GPU work; with PCS_BENCH_BACKEND=gloo it runs on a host without GPUs)')
     args = ap.parse_args()
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
     # PCS_BENCH_BACKEND=gloo + several ranks on one GPU: a rehearsal of the N > 1 code path on a
     # one-GPU box (host-staged transport; the timing is not a scaling number)
     backend = os.environ.get('PCS_BENCH_BACKEND', 'nccl')
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N ranks ourselves (before anything touches the GPU)
+        sys.exit(self_launch(args, backend))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    check_world(args, world, backend)
+    if args.launch_check:
+        sys.exit(launch_check(args, world, rank, backend))
     if backend != 'nccl':
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -684,7 +789,12 @@ def main():
 
     out = None
     if world > 1 or args.engine == 'slab':
-        res = slab_bench(n, dtype, K, W, world)
+        # the first multi-rank RCCL run must not lose the line: a stall prints it with an error
+        timer = headline_watchdog(args, rank, world, dtype)
+        try:
+            res = slab_bench(n, dtype, K, W, world)
+        finally:
+            timer.cancel()
         res['kernel_ms_isolated'] = res['kernel_ms']
     else:
         t0 = time.perf_counter()
@@ -695,9 +805,11 @@ def main():
         assert spec is not None and spec['fkind'] == 2, 'C3 problem must take the fused separable engine'
         res = fused_2d(pds, dtype, K, W)
         del pds
-        # the step kernel's mean duration: an event pair around each of 100 isolated launches
-        # (rocprofv3 kernel-trace average in profiles/ agrees); ms_per_step is the whole loop
-        res['kernel_ms'] = res['kernel_ms_isolated'] = res['kernels_ms']['step']
+        # one kernel per iteration, launched back to back from C: the step kernel's duration is
+        # the timed region's HIP-event time / K (inter-launch gaps included, so it never exceeds
+        # ms_per_step); the median of isolated event pairs is reported beside it
+        res['kernel_ms'] = res['ms_per_step']
+        res['kernel_ms_isolated'] = res['kernels_ms']['step']
         res['lipschitz'] = lips
         res['setup_s'] = round(setup, 2)
 
@@ -737,7 +849,11 @@ def main():
                                     'N = Conv^T Conv as two 29-tap passes)' if nm else
                                     'pcs_pds2d_step (k_pds2d_march<float,7,L21,256>)'),
                          'kernel_ms': round(res['kernel_ms'], 5),
-                         'kernel_ms_source': 'median of HIP-event pairs around each of 100 isolated launches',
+                         'kernel_ms_source': ('HIP events on the launch stream around the K back-to-back launches '
+                                              'of the timed region, / K (one kernel per iteration)'
+                                              if world == 1 and args.engine != 'slab' else
+                                              'mean of HIP-event pairs around isolated slab steps'),
+                         'kernel_ms_isolated_median': round(res['kernel_ms_isolated'], 5),
                          'alg_bytes_per_launch': alg_bytes,
                          # the 15x15 PSF work beside the bandwidth figure -- per pixel the
                          # normal operator's two 29-tap passes (nmarch) or the four 15-tap separable
@@ -749,7 +865,7 @@ def main():
         }
         if 'loop' in res:  # multi-GPU: which slab loop ran (native RCCL loop, or the torch.distributed fallback)
             out['loop'] = res['loop']
-            out['loop_fallback'] = res['loop'] == 'python'
+            out['loop_fallback'] = res['loop_fallback']
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:

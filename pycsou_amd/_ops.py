@@ -346,6 +346,17 @@ class FFTConv2D:
         if x.dtype != self.dtype:
             raise ValueError('FFTConv2D: dtype mismatch')
         out = torch.empty_like(x) if out is None else out
+        n = self.dims[0] * self.dims[1]
+        dev = torch.device('cuda', torch.cuda.current_device())
+        for name, t in (('x', x), ('out', out), ('b', b)):
+            if t is None:
+                continue
+            # the kernels read / write n0*n1 elements through raw pointers: validate before the call
+            if not isinstance(t, torch.Tensor) or t.dtype != self.dtype or t.numel() != n or not t.is_contiguous() \
+                    or t.device != dev:
+                raise ValueError(f'FFTConv2D.apply: {name} must be a contiguous {self.dtype} tensor of {n} elements '
+                                 f'on {dev} (got {getattr(t, "dtype", type(t))}, '
+                                 f'{getattr(t, "numel", lambda: "?")()} elements on {getattr(t, "device", "?")})')
         L.check(self._lib.pcs_fftconv2d_apply(self.handle, L.ptr(x), L.ptr(out), int(bool(adjoint)), L.ptr(b),
                                               float(beta), L.stream()), 'pcs_fftconv2d_apply')
         return out

@@ -32,10 +32,14 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     The run stops when r <= tol |theta|, when theta moved by at most ``tol`` (relative) since
     the previous check, or on an invariant subspace (beta ~ 0).
 
-    Returns theta + r: a Ritz value never exceeds the extreme eigenvalue, and some eigenvalue lies
-    within r of it, so the sum is an upper estimate of the extreme eigenvalue (the one the Ritz
-    value approximates) -- PDS step sizes built from it stay inside tau sigma ||K||^2 <= 1
-    (pycsou/opt/proxalgs.py:280-301) instead of exceeding it by the Ritz value's deficit."""
+    Returns theta + r when the residual test stopped the run (r <= tol |theta|: some eigenvalue lies
+    within r of the Ritz value, so the value errs by at most tol on the high side -- no guaranteed
+    upper bound on the extreme eigenvalue, since that eigenvalue need not be the one near theta),
+    and theta itself when it stopped on stagnation or an invariant subspace (a Ritz value never
+    exceeds the extreme eigenvalue; stagnation to tol means it is within about tol of it).  The
+    structured operators of the path (Gradient, derivatives, separable / 1-D convolutions) do not
+    come here: their norms are exact (linop/_spectral.py).
+    """
     from scipy.linalg import eigh_tridiagonal, eigvalsh_tridiagonal
     dev = O.device()
     g = torch.Generator(device='cpu').manual_seed(seed)
@@ -76,9 +80,12 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
             resid = 0.0 if bad.size else float(abs(be[k - 1] * S[-1, 0]))
         else:
             theta, resid = (float(abs(al[0])) if sym else float(al[0])), (0.0 if bad.size else float(abs(be[0])))
-        if (bad.size or resid <= tol * abs(theta)
-                or (prev is not None and abs(theta - prev) <= tol * abs(theta))):
-            break
+        if bad.size:
+            return theta
+        if resid <= tol * abs(theta):
+            return theta + resid
+        if prev is not None and abs(theta - prev) <= tol * abs(theta):
+            return theta
         prev = theta
     return theta + resid
 
@@ -173,8 +180,9 @@ class LinearOperator(DifferentiableMap):
         with k=1) by device Lanczos on ``K^T K`` (or ``|eig|`` if symmetric) in bounded memory
         (a few vectors of the domain size, whatever the operator's size).  Other ARPACK keyword
         arguments are accepted and ignored; ``tol`` is the relative residual (or change of the
-        estimate between checks) at which the iteration stops.  The value is an upper estimate
-        (Ritz value + residual bound, see _lanczos_extreme), so step sizes from it are safe."""
+        estimate between checks) at which the iteration stops; the value is accurate to about
+        ``tol`` relative (see _lanczos_extreme).  Structured operators override this with their
+        exact norms (linop/_spectral.py)."""
         if self.is_symmetric:
             lam = _lanczos_extreme(lambda v: self._apply(v), self.shape[1], sym=True, tol=tol, max_steps=max_steps)
             self.lipschitz_cst = float(abs(lam))
@@ -287,6 +295,24 @@ class LinOpComp(LinearOperator, DiffMapComp):
 
     def _jacT(self, t=None):
         return self.get_adjointOp()
+
+    def _factors(self):
+        out = []
+        for op in (self.LinOp1, self.LinOp2):
+            out.extend(op._factors() if isinstance(op, LinOpComp) else [op])
+        return out
+
+    def compute_lipschitz_cst(self, **kwargs):
+        """A composition of Convolve1D along distinct axes of one shape (the reference's only 3-D
+        blur, pycsou/linop/conv.py:20-164) is a Kronecker product: its norm is the product of the
+        factors' exact norms.  Anything else: the device Lanczos."""
+        from ..linop.conv import Convolve1DOp
+        f = self._factors()
+        if all(isinstance(o, Convolve1DOp) for o in f) and len({o.dims for o in f}) == 1 \
+                and len({o.axis for o in f}) == len(f):
+            self.lipschitz_cst = self.diff_lipschitz_cst = float(np.sqrt(np.prod([o.norm2() for o in f])))
+            return
+        LinearOperator.compute_lipschitz_cst(self, **kwargs)
 
 
 class SymmetricLinearOperator(LinearOperator):

@@ -20,6 +20,7 @@ import torch
 
 from .. import _ops as O
 from ..core.linop import LinearOperator
+from . import _spectral as S
 
 
 def pycsou_offset(n):
@@ -109,6 +110,22 @@ class Convolve2DOp(LinearOperator):
         t1[half - self.off[1]: half - self.off[1] + self.kw] = r
         return t0, t1, half
 
+    def compute_lipschitz_cst(self, **kwargs):
+        """||Conv||: a rank-1 PSF h = c r^T makes Conv = C_0 (x) C_1 (two 1-D 'same' convolutions at
+        pycsou's offsets), so ||Conv|| = ||C_0|| ||C_1||, each exact from its banded Gram matrix
+        (linop/_spectral.py); other PSFs keep the device Lanczos (core/linop.py).  Replaces the
+        reference's ARPACK svds (pycsou/core/linop.py:279-321)."""
+        u, s, vt = np.linalg.svd(self.filter)
+        if s[0] > 0 and (s.size == 1 or s[1] <= 1e-13 * s[0]):
+            c, r = u[:, 0] * np.sqrt(s[0]), vt[0] * np.sqrt(s[0])
+            n0, n1 = self.dims
+            # + the rank-1 remainder's bound ||Conv_e|| <= sum |e| <= sqrt(kh kw) ||e||_F (safe side)
+            rest = float(np.sqrt(self.kh * self.kw * np.sum(s[1:] ** 2)))
+            self.lipschitz_cst = self.diff_lipschitz_cst = float(
+                np.sqrt(S.conv1d_norm2(n0, c, self.off[0]) * S.conv1d_norm2(n1, r, self.off[1]))) + rest
+            return
+        LinearOperator.compute_lipschitz_cst(self, **kwargs)
+
 
 def Convolve2D(size, filter, shape, dtype='float64', method='fft'):
     """``pycsou/linop/conv.py:167-295``."""
@@ -135,6 +152,15 @@ class Convolve1DOp(LinearOperator):
 
     def _adj(self, t):
         return O.conv1d(t, self.dims, self.axis, self._hf.get(t.dtype), self.k, self.k - 1 - self.off)
+
+    def norm2(self):
+        """||Conv1D||^2 exactly: the 1-D banded Gram matrix along the axis (linop/_spectral.py)."""
+        return S.conv1d_norm2(self.dims[self.axis], self.filter, self.off)
+
+    def compute_lipschitz_cst(self, **kwargs):
+        """Exact ||Conv1D|| (K = I (x) C (x) I), in place of the reference's ARPACK svds
+        (pycsou/core/linop.py:279-321)."""
+        self.lipschitz_cst = self.diff_lipschitz_cst = float(np.sqrt(self.norm2()))
 
 
 def Convolve1D(size, filter, reshape_dims=None, axis=0, dtype='float64', method=None):

@@ -14,6 +14,7 @@ import numpy as np
 
 from .. import _ops as O
 from ..core.linop import LinearOperator
+from . import _spectral as S
 
 
 def _steps(step, nd):
@@ -51,6 +52,12 @@ class FirstDerivativeOp(_DiffOp):
     def _adj(self, t):
         return O.deriv1(t, self.dims, self.axis, self.step, self.kind, self.edge, adjoint=True)
 
+    def compute_lipschitz_cst(self, **kwargs):
+        """Exact ||D|| = sqrt(lambda_max(D_1^T D_1)) of the 1-D stencil along the axis (K = I (x) D_1 (x) I;
+        linop/_spectral.py), in place of the reference's ARPACK svds (pycsou/core/linop.py:279-321)."""
+        self.lipschitz_cst = self.diff_lipschitz_cst = float(
+            np.sqrt(S.deriv1_norm2(self.dims[self.axis], self.kind, self.edge, self.step)))
+
 
 def FirstDerivative(size, shape=None, axis=0, step=1.0, edge=True, dtype='float64', kind='forward'):
     """``pycsou/linop/diff.py:24-130``."""
@@ -75,6 +82,14 @@ class GradientOp(_DiffOp):
 
     def _adj(self, t):
         return O.grad_adj(t, self.dims, self.steps, self.kind, self.edge)
+
+    def compute_lipschitz_cst(self, **kwargs):
+        """Exact ||K||: K^T K = sum_k I (x) D_k^T D_k (x) I is a Kronecker sum, so ||K||^2 = sum_k
+        lambda_max(D_k^T D_k) over the 1-D stencils of the axes (linop/_spectral.py; forward /
+        backward: 4 sin^2(pi (n-1) / 2n) / h^2 per axis), in place of the reference's ARPACK svds
+        (pycsou/core/linop.py:279-321)."""
+        self.lipschitz_cst = self.diff_lipschitz_cst = float(np.sqrt(sum(
+            S.deriv1_norm2(n, self.kind, self.edge, h) for n, h in zip(self.dims, self.steps))))
 
 
 def Gradient(shape, step=1., edge=True, dtype='float64', kind='centered'):
@@ -122,6 +137,11 @@ class SecondDerivativeOp(_DiffOp):
 
     def _adj(self, t):
         return O.deriv2(t, self.dims, self.axis, self.step, self.edge, adjoint=True)
+
+    def compute_lipschitz_cst(self, **kwargs):
+        """Exact ||D2|| of the 1-D second-difference stencil along the axis (linop/_spectral.py)."""
+        self.lipschitz_cst = self.diff_lipschitz_cst = float(
+            np.sqrt(S.deriv2_norm2(self.dims[self.axis], self.edge, self.step)))
 
 
 def SecondDerivative(size, shape=None, axis=0, step=1.0, edge=True, dtype='float64'):

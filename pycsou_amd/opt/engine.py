@@ -417,7 +417,12 @@ class PDS2DEngine:
             ev[name].append((e0, e1))
         for i in range(n):
             p = i % 2
-            if self.fkind == L.PCS_F_GRADBUF:
+            if self.fkind == L.PCS_F_GRADBUF and (self.plans[0] is None or self.plans[1] is None):
+                # PSF wider than the direct tiers: the FFT-domain plan's two passes
+                f = self.conv.fft(self.dtype)
+                timed('conv_fwd', lambda: f.apply(self.X[p], b=self.y, beta=-1.0, out=self.R))
+                timed('conv_adj', lambda: f.apply(self.R, adjoint=True, out=self.Gb))
+            elif self.fkind == L.PCS_F_GRADBUF:
                 fwd, adj = self.plans
                 n0, n1 = self.conv.dims
                 timed('conv_fwd', lambda: L.check(lib.pcs_conv2d_planned(

@@ -408,6 +408,11 @@ class SlabPDS2D:
             self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
             a.gbuf, a.x, a.xn, a.z, a.zn, a.partials = saved
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
+        if self.nblocks < 0:
+            kname = {L.PCS_K_GRAD_FORWARD: 'forward Gradient', L.PCS_K_GRAD_BACKWARD: 'backward Gradient',
+                     L.PCS_K_GRAD_CENTERED: 'centered Gradient', L.PCS_K_LAPLACIAN: 'Laplacian'}.get(kk, str(kk))
+            raise ValueError(f'row-slab PDS: no fused slab kernel for K = {kname}, dtype {dtype}, image {n0}x{n1} '
+                             f'(F mode {mode!r}); run this problem on one GPU (PDS.iterate)')
         self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
         a.partials = self.partials.data_ptr()
         a.hist, a.ws = None, None

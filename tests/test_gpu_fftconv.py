@@ -54,6 +54,64 @@ def test_fftconv_vs_reference(shape, k, dtype):
     assert rel(adj, adj_ref) < tol, rel(adj, adj_ref)
 
 
+@pytest.mark.parametrize('block', [64, 100])
+@pytest.mark.parametrize('shape, k', [((300, 260), (63, 63)), ((257, 1000), (33, 47)), ((96, 70), (64, 40))])
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+def test_fftconv_blocked_vs_reference(shape, k, dtype, block, monkeypatch):
+    """The overlap-add block path (the default once an axis exceeds 2048 samples, e.g. 4096^2):
+    PCS_FFT_BLOCK set small when the plan is created, so 2 x 2 and larger block grids with uneven
+    last blocks run -- multi-block pad, the crop's block-candidate sums, the adjoint's negative
+    offsets -- forward and adjoint against the oracle."""
+    from pycsou_amd.linop.conv import Convolve2D
+    monkeypatch.setenv('PCS_FFT_BLOCK', str(block))
+    h = _psf(*k, seed=k[0] + 1)
+    N = shape[0] * shape[1]
+    C = Convolve2D(N, h, shape)  # plan created below, with the block override in the environment
+    x = np.random.default_rng(4).standard_normal(N)
+    ref_op = P.Convolve2D(N, h, shape, offset=tuple(P.pycsou_offset(n) for n in k))
+    xd = torch.as_tensor(x.astype(dtype)).cuda()
+    fwd = C(xd).cpu().numpy()
+    adj = C.adjoint(xd).cpu().numpy()
+    tol = 1e-12 if dtype == np.float64 else 3e-6
+    assert rel(fwd, ref_op.matvec(x)) < tol, rel(fwd, ref_op.matvec(x))
+    assert rel(adj, ref_op.rmatvec(x)) < tol, rel(adj, ref_op.rmatvec(x))
+    # residual form through the blocks too
+    y = torch.as_tensor(np.random.default_rng(5).standard_normal(N).astype(dtype)).cuda()
+    r = C._apply_minus(xd, y).cpu().numpy()
+    assert rel(r, fwd - y.cpu().numpy()) < tol
+
+
+@pytest.mark.parametrize('block', [64, 100])
+def test_fftconv_blocked_adjoint_dot_test(block, monkeypatch):
+    from pycsou_amd.linop.conv import Convolve2D
+    monkeypatch.setenv('PCS_FFT_BLOCK', str(block))
+    shape, h = (130, 190), _psf(63, 35, seed=3)
+    N = shape[0] * shape[1]
+    C = Convolve2D(N, h, shape)
+    rng = np.random.default_rng(2)
+    u, v = torch.as_tensor(rng.standard_normal(N)).cuda(), torch.as_tensor(rng.standard_normal(N)).cuda()
+    lhs = float(torch.dot(C(u), v))
+    rhs = float(torch.dot(u, C.adjoint(v)))
+    assert abs(lhs - rhs) <= 1e-12 * max(abs(lhs), 1.0)
+
+
+def test_fftconv_apply_validates_buffers():
+    """A wrong-length, non-contiguous or wrong-dtype buffer is a ValueError before any device call."""
+    from pycsou_amd.linop.conv import Convolve2D
+    shape = (64, 80)
+    N = shape[0] * shape[1]
+    f = Convolve2D(N, _psf(41, 41, seed=1), shape).fft(torch.float64)
+    x = torch.zeros(N, dtype=torch.float64, device='cuda')
+    with pytest.raises(ValueError):
+        f.apply(torch.zeros(N - 1, dtype=torch.float64, device='cuda'))
+    with pytest.raises(ValueError):
+        f.apply(x, out=torch.zeros(2 * N, dtype=torch.float64, device='cuda')[::2])
+    with pytest.raises(ValueError):
+        f.apply(x, b=torch.zeros(N + 4, dtype=torch.float64, device='cuda'), beta=-1.0)
+    with pytest.raises(ValueError):
+        f.apply(x, out=torch.zeros(N, dtype=torch.float32, device='cuda'))
+
+
 def test_fftconv_adjoint_dot_test():
     from pycsou_amd.linop.conv import Convolve2D
     shape, h = (130, 190), _psf(63, 35, seed=3)

@@ -77,6 +77,27 @@ def test_slab_rejects_thin():
         SlabPDS2D.from_pds(pds, None, rank=0, world=8)  # 8 rows < 15-row halo
 
 
+@pytest.mark.parametrize('shape', [(64, 66), (96, 60)])
+def test_slab_rejects_unsupported_kernel(shape):
+    """A problem no fused slab kernel takes (centred K on an fp32 image whose rows are not 16-B
+    groups, or narrower than two 64-column strips) is a ValueError naming K, dtype and shape --
+    not a negative-size allocation."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.proxalgs import PDS
+    from pycsou_amd.parallel import SlabPDS2D
+    N = shape[0] * shape[1]
+    K = Gradient(shape, kind='centered')
+    K.lipschitz_cst = K.diff_lipschitz_cst = 2.0
+    y = np.random.default_rng(0).uniform(0, 1, N).astype(np.float32)
+    pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y), H=0.1 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)),
+              K=K, x0=np.zeros(N, np.float32), z0=np.zeros(2 * N, np.float32), max_iter=4, min_iter=4,
+              accuracy_threshold=0.0, verbose=None)
+    with pytest.raises(ValueError, match=r'centered Gradient.*float32'):
+        SlabPDS2D.from_pds(pds, None, rank=0, world=2)
+
+
 def _synth_single_and_slabs(name, world):
     """(single-GPU fused engine result, run_local slabs result) of a slab_worker.SYNTH problem."""
     from pycsou_amd.parallel import SlabPDS2D, run_local
