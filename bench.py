@@ -487,6 +487,49 @@ def leg_c3_cen(args, dtype, K, W):
     return res
 
 
+def leg_c3_f64(args, dtype, K, W, kind='forward'):
+    """C3 at the reference's default precision, fp64 (x0 / z0 np.float, pycsou/opt/proxalgs.py:327,341;
+    Gradient / Convolve2D dtype='float64', linop/diff.py:777, linop/conv.py:167): 4096^2, the same
+    separable 15x15 blur.  fp64 takes the general-stencil engine's fp64 row march for every K kind:
+    N x = Conv^T Conv x by k_sep2d_nrm<double> into a buffer (2 words), then the march step
+    (k_pds2d_smarch<double>: reads x, N x, Conv^T y, z; writes x', z' -- 8 words).  Algorithmic bytes
+    of the iteration: 7 words x 8 B per pixel."""
+    n = args.size
+    dt = torch.float64
+    t0 = time.perf_counter()
+    pds = build_problem(n, n, dt, lipschitz=args.lipschitz, kind=kind)
+    setup = time.perf_counter() - t0
+    r = fused_2d(pds, dt, K, W)
+    del pds
+    N = n * n
+    alg = 7 * N * 8
+    km = r['kernels_ms']
+    res = {'workload': f'C3 TV-deconvolution {n}x{n} f64 (the reference default dtype), 15x15 Gaussian PSF (separable), '
+                       f'K = Gradient(kind={kind}), 0.05*L21Norm; grad F = N x - Conv^T y: N x by k_sep2d_nrm<double> '
+                       f'into a buffer + the fp64 general-stencil march step (k_pds2d_smarch<double>), back to back from C',
+           'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
+           'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'dtype': 'f64',
+           'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
+           'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if 'conv_nx' in km:
+        upd = km['step'] - km['conv_nx']
+        step_bytes = 8 * N * 8
+        res['roofline'] = {'bound': 'hbm', 'kernel': f'k_pds2d_smarch<double, {kind}, NB, L21> (update)',
+                           'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
+                           'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        res['nx_roofline'] = {'bound': 'hbm', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm<double>)',
+                              'kernel_ms': round(km['conv_nx'], 5), 'bytes_per_launch': 2 * N * 8,
+                              'achieved': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9, 1),
+                              'frac': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return res
+
+
+def leg_c3_cen_f64(args, dtype, K, W):
+    """leg_c3_f64 with the reference's default K = Gradient(shape) (centred, edge=True)."""
+    return leg_c3_f64(args, dtype, K, W, kind='centered')
+
+
 def leg_conv63(args, dtype, K, W):
     """Convolve2D with a 63 x 63 non-separable PSF on a 4096^2 image (the reference's default
     method='fft', pycsou/linop/conv.py:209-217, 294): one forward and one adjoint pass through the
@@ -747,7 +790,7 @@ def main():
     ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10,c4_cen:512:f32:20:centered',
                     help='volume legs name:edge:dtype:steps[:kind], comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
-    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,conv63,cps_inpaint',
+    ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,c3_f64,c3_cen_f64,conv63,cps_inpaint',
                     help='single-GPU 2-D legs after the headline: c2 (2048^2 denoising), c3_nonsep (non-separable '
                          'PSF), c2_lap / c2_cen (Laplacian / centered-Gradient K), c3_cen (C3 with the default '
                          'centered Gradient), conv63 (63x63 FFT Convolve2D), cps_inpaint (generic path); "" skips them')
@@ -873,7 +916,8 @@ def main():
         if world == 1 and args.engine != 'slab':
             for leg in filter(None, args.legs.split(',')):
                 fn = {'c2': leg_c2, 'c3_nonsep': leg_c3_nonsep, 'c2_lap': leg_c2_lap, 'c2_cen': leg_c2_cen,
-                      'c3_cen': leg_c3_cen, 'conv63': leg_conv63, 'cps_inpaint': leg_cps_inpaint}[leg]
+                      'c3_cen': leg_c3_cen, 'c3_f64': leg_c3_f64, 'c3_cen_f64': leg_c3_cen_f64, 'conv63': leg_conv63,
+                      'cps_inpaint': leg_cps_inpaint}[leg]
                 try:
                     out[leg] = fn(args, dtype, K, W)
                 except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own

@@ -428,6 +428,7 @@ static bool sm_forward() {
   return e != nullptr && atoi(e) != 0;
 }
 
+template <typename T>
 static int sm_slots() {
   static int slots = 0;
   if (slots == 0) {
@@ -435,10 +436,10 @@ static int sm_slots() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_smarch<PCS_CENTERED, PCS_F_DENOISE, PCS_H_L21>, 256,
-                                                     0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_smarch<T, PCS_CENTERED, PCS_F_DENOISE, PCS_H_L21>,
+                                                     256, 0) != hipSuccess ||
         nb < 1)
-      nb = 3;
+      nb = sizeof(T) == 4 ? 3 : 2;
     (void)hipGetLastError();
     slots = cus * (nb < 3 ? nb : 3);  // as the pt kernel: fewer, longer row segments
     const char* e = getenv("PCS_SM_SLOTS");  // diagnostics: grid-size sweep
@@ -450,7 +451,7 @@ static int sm_slots() {
 static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tiles_x = (int)((a->n1 + 63) / 64);
   if (tiles_x < 2) return false;
-  plan_bands(rb, 16, tiles_x, sm_slots(), 4, p);
+  plan_bands(rb, 16, tiles_x, a->dtype == PCS_F64 ? sm_slots<double>() : sm_slots<float>(), 4, p);
   return true;
 }
 
@@ -469,93 +470,104 @@ static bool sm_normal(const pcs_pds2d_args* a) {
   int64_t lo, hi;
   window_rows(a, a->halo_x, &lo, &hi);
   // shape / tap validation only (nplanes 0): any non-null input will do before x is bound
-  return pcs_conv2d_sep_ata_planes(PCS_F32, a->x ? a->x : a->cty, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1,
+  return pcs_conv2d_sep_ata_planes(a->dtype, a->x ? a->x : a->cty, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1,
                                    a->taps0, 2 * a->half + 1, a->half, a->taps1, 2 * a->half + 1, a->half,
                                    nullptr) == PCS_OK;
 }
 
 static bool use_march(const pcs_pds2d_args* a);
 
+// fp64 (the reference's default dtype): every K kind, the forward Gradient included, takes this march
+// (the forward-only fp32 kernels pds_pt.hpp / pds_nmarch.hpp have no fp64 form)
 static bool use_smarch(const pcs_pds2d_args* a) {
-  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward()) return false;
+  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward() && a->dtype != PCS_F64) return false;
   // separable PSF with backward / centred K: the fused normal-operator march (one launch) when it applies
   if (a->kkind != PCS_K_GRAD_FORWARD && a->fkind == PCS_F_SEPCONV && use_march(a)) return false;
   if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return false;
-  if (a->dtype != PCS_F32 || !make_slab(a).vec) return false;
+  if ((a->dtype != PCS_F32 && a->dtype != PCS_F64) || !make_slab(a).vec) return false;
   if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF &&
-      !(a->kkind != PCS_K_GRAD_FORWARD && sm_normal(a)))
+      !((a->kkind != PCS_K_GRAD_FORWARD || a->dtype == PCS_F64) && sm_normal(a)))
     return false;
   if (a->hkind != PCS_H_L1 && (a->hkind != PCS_H_L21 || a->kkind == PCS_K_LAPLACIAN)) return false;
   const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
                                              : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
-  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
+  const int64_t esz = a->dtype == PCS_F64 ? 8 : 4;
+  // 32-bit indexing; every buffer view (z: one per component) at most 2^30 bytes (kOOB)
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * esz <= (1LL << 30))) return false;
   MarchPlan p;
   return sm_plan(a, full_bands(a), &p);
 }
 
-static SParams make_sparams(const pcs_pds2d_args* a) {
-  SParams Q;
-  Q.ih20 = (float)(1.0 / (a->step0 * a->step0));
-  Q.ih21 = (float)(1.0 / (a->step1 * a->step1));
-  Q.w0 = (float)a->w0;
-  Q.w1 = (float)a->w1;
+template <typename T>
+static SParamsT<T> make_sparams(const pcs_pds2d_args* a) {
+  SParamsT<T> Q;
+  Q.ih20 = (T)(1.0 / (a->step0 * a->step0));
+  Q.ih21 = (T)(1.0 / (a->step1 * a->step1));
+  Q.w0 = (T)a->w0;
+  Q.w1 = (T)a->w1;
   Q.edge = a->edge != 0;
   return Q;
 }
 
-template <int KK, int FK, int HK>
+template <typename T, int KK, int FK, int HK>
 static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   MarchPlan p;
   if (!sm_plan(a, rb, &p)) return PCS_EINVAL;
   if (p.ntasks == 0) return PCS_OK;
   const Slab s64 = make_slab(a);
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
-  const Params<float> P = make_params<float>(a);
-  const float* g = FK == PCS_F_DENOISE                       ? (const float*)a->y
-                   : (FK == PCS_F_GRADBUF || FK == SM_F_NB) ? (const float*)a->gbuf
-                                                            : nullptr;
-  const float* b = FK == SM_F_NB ? (const float*)a->cty : nullptr;
-  k_pds2d_smarch<KK, FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
-      (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, g, b, s, P, make_sparams(a), a->gkind,
-      a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
+  const Params<T> P = make_params<T>(a);
+  const T* g = FK == PCS_F_DENOISE                       ? (const T*)a->y
+               : (FK == PCS_F_GRADBUF || FK == SM_F_NB) ? (const T*)a->gbuf
+                                                        : nullptr;
+  const T* b = FK == SM_F_NB ? (const T*)a->cty : nullptr;
+  k_pds2d_smarch<T, KK, FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
+      (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, s, P, make_sparams<T>(a), a->gkind, a->partials,
+      (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
   return launch_status();
 }
 
-template <int KK, int FK>
+template <typename T, int KK, int FK>
 static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  if constexpr (KK == SK_LAP) return launch_smarch<KK, FK, PCS_H_L1>(a, rb, st);
+  if constexpr (KK == SK_LAP) return launch_smarch<T, KK, FK, PCS_H_L1>(a, rb, st);
   else
-    return a->hkind == PCS_H_L21 ? launch_smarch<KK, FK, PCS_H_L21>(a, rb, st)
-                                 : launch_smarch<KK, FK, PCS_H_L1>(a, rb, st);
+    return a->hkind == PCS_H_L21 ? launch_smarch<T, KK, FK, PCS_H_L21>(a, rb, st)
+                                 : launch_smarch<T, KK, FK, PCS_H_L1>(a, rb, st);
 }
 
-template <int KK>
+template <typename T, int KK>
 static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   if (a->fkind == PCS_F_SEPCONV) {  // N x -> gbuf on the stored rows (clipped to the image), then the
-    // step with grad F = gbuf - cty; whole slabs only (the N x pass runs once per iteration)
-    if (KK == PCS_FORWARD || rb.ra0 != 0 || rb.rb0 != a->rows) return PCS_EUNSUPPORTED;
+    // step with grad F = gbuf - cty; whole slabs only (the N x pass runs once per iteration).  The
+    // forward Gradient comes here in fp64 only (fp32 has the fused normal-operator march)
+    if ((KK == PCS_FORWARD && sizeof(T) == 4) || rb.ra0 != 0 || rb.rb0 != a->rows) return PCS_EUNSUPPORTED;
     int64_t lo, hi;
     window_rows(a, a->halo_x, &lo, &hi);
     const int64_t off = (lo + a->halo_x) * a->n1;
-    const int rc = pcs_conv2d_sep_ata_planes(PCS_F32, (const float*)a->x + off, (float*)const_cast<void*>(a->gbuf) + off,
-                                             1, hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half, a->taps1,
+    const int rc = pcs_conv2d_sep_ata_planes(a->dtype, (const T*)a->x + off, (T*)const_cast<void*>(a->gbuf) + off, 1,
+                                             hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half, a->taps1,
                                              2 * a->half + 1, a->half, st);
     if (rc != PCS_OK) return rc;
-    return launch_smarch<KK, SM_F_NB>(a, rb, st);
+    return launch_smarch<T, KK, SM_F_NB>(a, rb, st);
   }
-  if (a->fkind == PCS_F_DENOISE) return launch_smarch<KK, PCS_F_DENOISE>(a, rb, st);
-  if (a->fkind == PCS_F_GRADBUF) return launch_smarch<KK, PCS_F_GRADBUF>(a, rb, st);
-  return launch_smarch<KK, PCS_F_NULL>(a, rb, st);
+  if (a->fkind == PCS_F_DENOISE) return launch_smarch<T, KK, PCS_F_DENOISE>(a, rb, st);
+  if (a->fkind == PCS_F_GRADBUF) return launch_smarch<T, KK, PCS_F_GRADBUF>(a, rb, st);
+  return launch_smarch<T, KK, PCS_F_NULL>(a, rb, st);
+}
+
+template <typename T>
+static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  switch (a->kkind) {
+    case PCS_K_GRAD_FORWARD: return launch_smarch<T, PCS_FORWARD>(a, rb, st);
+    case PCS_K_GRAD_BACKWARD: return launch_smarch<T, PCS_BACKWARD>(a, rb, st);
+    case PCS_K_GRAD_CENTERED: return launch_smarch<T, PCS_CENTERED>(a, rb, st);
+    case PCS_K_LAPLACIAN: return launch_smarch<T, SK_LAP>(a, rb, st);
+    default: return PCS_EINVAL;
+  }
 }
 
 static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  switch (a->kkind) {
-    case PCS_K_GRAD_FORWARD: return launch_smarch<PCS_FORWARD>(a, rb, st);
-    case PCS_K_GRAD_BACKWARD: return launch_smarch<PCS_BACKWARD>(a, rb, st);
-    case PCS_K_GRAD_CENTERED: return launch_smarch<PCS_CENTERED>(a, rb, st);
-    case PCS_K_LAPLACIAN: return launch_smarch<SK_LAP>(a, rb, st);
-    default: return PCS_EINVAL;
-  }
+  return a->dtype == PCS_F64 ? launch_smarch<double>(a, rb, st) : launch_smarch<float>(a, rb, st);
 }
 
 // the row-marching families (march, pt, smarch) take row bands; the tile kernel runs whole slabs only

@@ -135,6 +135,51 @@ __device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, const G4<float>& g
   __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)off, 0, AUX);
 }
 
+// Element-typed forms for kernels templated on the element type: a 4-column group is one 16-B
+// access in fp32 and two (off, off + 16) in fp64; a single element is a b32 / b64 access.  A kOOB
+// offset stays out of range in the second half too (kOOB + 16 < 2^31 is still >= every size).
+template <typename T>
+__device__ __forceinline__ G4<T> bload4t(Rsrc r, uint32_t off);
+template <>
+__device__ __forceinline__ G4<float> bload4t<float>(Rsrc r, uint32_t off) {
+  return bload4(r, off);
+}
+template <>
+__device__ __forceinline__ G4<double> bload4t<double>(Rsrc r, uint32_t off) {
+  const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off + 16u), 0, 0);
+  G4<double> g;
+  __builtin_memcpy(&g.v[0], &a, 16);
+  __builtin_memcpy(&g.v[2], &b, 16);
+  return g;
+}
+template <typename T>
+__device__ __forceinline__ T bload1t(Rsrc r, uint32_t off);
+template <>
+__device__ __forceinline__ float bload1t<float>(Rsrc r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+template <>
+__device__ __forceinline__ double bload1t<double>(Rsrc r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  double d;
+  __builtin_memcpy(&d, &v, 8);
+  return d;
+}
+template <typename T, int AUX = 0>
+__device__ __forceinline__ void bstore4t(Rsrc r, uint32_t off, const G4<T>& g) {
+  if constexpr (sizeof(T) == 4) {
+    bstore4<AUX>(r, off, g);
+  } else {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    u4 a, b;
+    __builtin_memcpy(&a, &g.v[0], 16);
+    __builtin_memcpy(&b, &g.v[2], 16);
+    __builtin_amdgcn_raw_buffer_store_b128(a, r, (int)off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(b, r, (int)(off + 16u), 0, AUX);
+  }
+}
+
 // Diagnostic ablation builds only (-DPCS_ABL=bits, tools/build_var.sh): 1 = z not landed in LDS,
 // 2 = y not parked, 4 = new x rows not stored, 8/16/32 = P1/P2/P3 skipped, 64/128 = P45/P6 reduced to
 // their stores, 256 = without those stores, 512 = no LDS barriers, 1024 = loads from 4 rows (L2-resident) and
@@ -167,18 +212,19 @@ struct View {
     return ((unsigned)(lr - lo) <= (unsigned)(hi - lo)) ? (uint32_t)(lr + halo) * pitch : kOOB;
   }
 };
-__device__ __forceinline__ View make_view(const void* base, const Slab32& s, int halo) {
+// esz: element size in bytes (4: fp32, 8: fp64)
+__device__ __forceinline__ View make_view(const void* base, const Slab32& s, int halo, uint32_t esz = 4u) {
   View v;
   v.halo = halo;
   v.lo = max(-halo, -s.row0);
   v.hi = min(s.rows + halo, s.n0 - s.row0) - 1;
-  v.pitch = (uint32_t)s.n1 * 4u;
+  v.pitch = (uint32_t)s.n1 * esz;
   v.r = rsrc_of(base, (uint32_t)(s.rows + 2 * halo) * v.pitch);
   return v;
 }
 // byte offset of column c inside a row (kOOB outside the image; 4-groups are wholly in/out)
-__device__ __forceinline__ uint32_t col_off(int c, int n1) {
-  return ((unsigned)c < (unsigned)n1) ? (uint32_t)c * 4u : kOOB;
+__device__ __forceinline__ uint32_t col_off(int c, int n1, uint32_t esz = 4u) {
+  return ((unsigned)c < (unsigned)n1) ? (uint32_t)c * esz : kOOB;
 }
 
 // A loop-invariant value re-materialised in a VGPR every step, so tests on it stay inside the

@@ -1,4 +1,4 @@
-// Row-marching fused 2-D PDS step for a GENERAL finite-difference K (fp32, pointwise grad F):
+// Row-marching fused 2-D PDS step for a GENERAL finite-difference K (fp32 / fp64, pointwise grad F):
 //   K = Gradient(kind = 'backward' | 'centered' | 'forward', edge, sampling)   (pycsou/linop/diff.py:777-882;
 //       'centered' is the reference's default), z = [D0 x; D1 x]
 //   K = Laplacian(weights, sampling, edge) = w0 D2_0 + w1 D2_1                (diff.py:885-957), z = K x
@@ -67,11 +67,13 @@ enum { SM_F_NB = 16 };
 
 // the stencils on a 5-sample window: stencil.hpp (sw_d1_fwd / sw_d1_adj / sw_d2_fwd / sw_d2_adj)
 
-// stencil-specific parameters (the rest is Params<float>)
-struct SParams {
-  float ih20, ih21, w0, w1;  // 1 / sampling^2 per axis, Laplacian weights
+// stencil-specific parameters (the rest is Params<T>)
+template <typename T>
+struct SParamsT {
+  T ih20, ih21, w0, w1;  // 1 / sampling^2 per axis, Laplacian weights
   int edge;
 };
+using SParams = SParamsT<float>;
 
 template <int KK>
 struct SMarch {
@@ -99,14 +101,16 @@ struct SMarch {
   static constexpr int O_Z = 0, O_U = D * RING * WZ, SZ = O_U + RING * WZ;
 };
 
-template <int KK, int FK, int HK, bool CI>
-__device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* __restrict__ xn,
-                                            const float* __restrict__ z, float* __restrict__ zn,
-                                            const float* __restrict__ gsrc, const float* __restrict__ bsrc,
-                                            const Slab32& s, const Params<float>& P,
-                                            const SParams& Q, int gk, int s0, int s1, int c0, float* sm,
+// T = float or double: the same geometry (4-column groups, 64-column strips, 16-row steps); an fp64
+// group is two 16-B accesses and the rings take twice the LDS (58 KB for a Gradient K)
+template <typename T, int KK, int FK, int HK, bool CI>
+__device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restrict__ xn,
+                                            const T* __restrict__ z, T* __restrict__ zn,
+                                            const T* __restrict__ gsrc, const T* __restrict__ bsrc,
+                                            const Slab32& s, const Params<T>& P,
+                                            const SParamsT<T>& Q, int gk, int s0, int s1, int c0, T* sm,
                                             double (&part)[4]) {
-  using T = float;
+  constexpr uint32_t ES = sizeof(T);
   using M = SMarch<KK>;
   constexpr int NT = 256, TS = M::TS, TW = M::TW, WZ = M::WZ, GZ = M::GZ, D = M::D, RING = M::RING;
   constexpr int KZ = cdiv(M::NZN, NT);
@@ -118,16 +122,16 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
   const int ui = 2 * hb + lane_grp(l5), ug = lane_idx(l5);  // both phases: row ui of the step, group ug
   const int n0 = s.n0, n1 = s.n1, edge = Q.edge;
   const int zstride = (s.rows + 2 * s.hz) * n1;
-  const View vx = make_view(x, s, s.hx), vg = make_view(gsrc != nullptr ? gsrc : x, s, s.hy),
-             vb = make_view(bsrc != nullptr ? bsrc : x, s, s.hy);
+  const View vx = make_view(x, s, s.hx, ES), vg = make_view(gsrc != nullptr ? gsrc : x, s, s.hy, ES),
+             vb = make_view(bsrc != nullptr ? bsrc : x, s, s.hy, ES);
   View vz[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) vz[d] = make_view(z + d * zstride, s, s.hz);
-  const uint32_t pitch = (uint32_t)n1 * 4u;
+  for (int d = 0; d < D; ++d) vz[d] = make_view(z + d * zstride, s, s.hz, ES);
+  const uint32_t pitch = (uint32_t)n1 * ES;
   const Rsrc rxn = rsrc_of(xn, (uint32_t)(s.rows + 2 * s.hx) * pitch);
   Rsrc rzn[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) rzn[d] = rsrc_of(zn + d * zstride, (uint32_t)zstride * 4u);
+  for (int d = 0; d < D; ++d) rzn[d] = rsrc_of(zn + d * zstride, (uint32_t)zstride * ES);
 #define PCS_WAVE_ON(k, N) ((k) * NT + wv * 64 < (N))
 #define PCS_ITEM(k, N) min((k) * NT + tid, (N) - 1)
 
@@ -145,7 +149,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
 #ifndef PCS_SM_E5
 #define PCS_SM_E5 1
 #endif
-  const uint32_t co_c = col_off(c, n1), co_e = (!PCS_SM_E5 || ext_st) ? col_off(ce, n1) : kOOB;
+  const uint32_t co_c = col_off(c, n1, ES), co_e = (!PCS_SM_E5 || ext_st) ? col_off(ce, n1, ES) : kOOB;
   // CI: the strip and its 4-column margins lie >= 2 columns inside the image (no column edge rule)
   const bool cin = CI || c < n1, ce_in = CI || (unsigned)ce < (unsigned)n1;
   uint32_t co_z[KZ];
@@ -155,7 +159,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     const int e = PCS_ITEM(k, M::NZN), g = e - (e / GZ) * GZ;
     rr_z[k] = e / GZ;
     lo_z[k] = 4 * g;
-    co_z[k] = col_off(c0 - 4 + 4 * g, n1);
+    co_z[k] = col_off(c0 - 4 + 4 * g, n1, ES);
   }
   // x, y|g (and b) of the U items in two register sets: the set of step k + 1 loads at the top of
   // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index)
@@ -171,7 +175,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
 #pragma unroll
       for (int k = 0; k < KZ; ++k) {
         const int r = a + M::ZHI - 15 + rr_z[k];
-        dst[d][k] = bload4(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
+        dst[d][k] = bload4t<T>(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
       }
   };
   auto land_z_from = [&](const G4<T>(&src)[D][KZ], int a) {
@@ -189,17 +193,17 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     constexpr int PB = decltype(pb)::value;
     const int r = a + 1 + ui;
     const uint32_t ro = r < rmin ? kOOB : vx.row_off(r);
-    xr[PB] = bload4(vx.r, ro + co_c);
-    xe[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vx.r, (int)(ro + co_e), 0, 0));
+    xr[PB] = bload4t<T>(vx.r, ro + co_c);
+    xe[PB] = bload1t<T>(vx.r, ro + co_e);
     if constexpr (FK != PCS_F_NULL) {
       const uint32_t rg = r < rmin ? kOOB : vg.row_off(r);
-      gr[PB] = bload4(vg.r, rg + co_c);
-      ge[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vg.r, (int)(rg + co_e), 0, 0));
+      gr[PB] = bload4t<T>(vg.r, rg + co_c);
+      ge[PB] = bload1t<T>(vg.r, rg + co_e);
     }
     if constexpr (FK == SM_F_NB) {
       const uint32_t rb = r < rmin ? kOOB : vb.row_off(r);
-      br[PB] = bload4(vb.r, rb + co_c);
-      be[PB] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(rb + co_e), 0, 0));
+      br[PB] = bload4t<T>(vb.r, rb + co_c);
+      be[PB] = bload1t<T>(vb.r, rb + co_e);
     }
   };
 
@@ -276,7 +280,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     T* urow = UR + (lr & 31) * WZ;
     st4(urow + lc, uo);
     if (ext_st) urow[lce] = ue;
-    bstore4<PCS_SM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
+    bstore4t<T, PCS_SM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
   };
 
   // ---- Z: z' on row lr = a + ui, columns c .. c + 3
@@ -345,7 +349,7 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
     }
     const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_c;
 #pragma unroll
-    for (int d = 0; d < D; ++d) bstore4<PCS_SM_SAUX>(rzn[d], off, o[d]);
+    for (int d = 0; d < D; ++d) bstore4t<T, PCS_SM_SAUX>(rzn[d], off, o[d]);
   };
 
   // prologue: u on rows [s0 - UPRO, s0] (a pseudo-step at a = s0 - TS whose loads skip the rows
@@ -407,15 +411,15 @@ __device__ __forceinline__ void smarch_task(const float* __restrict__ x, float* 
 #undef PCS_ITEM
 }
 
-template <int KK, int FK, int HK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE))) void k_pds2d_smarch(const float* __restrict__ x, float* __restrict__ xn,
-                                                       const float* __restrict__ z, float* __restrict__ zn,
-                                                       const float* __restrict__ gsrc,
-                                                       const float* __restrict__ bsrc, Slab32 s, Params<float> P,
-                                                       SParams Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
+template <typename T, int KK, int FK, int HK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE))) void k_pds2d_smarch(const T* __restrict__ x, T* __restrict__ xn,
+                                                       const T* __restrict__ z, T* __restrict__ zn,
+                                                       const T* __restrict__ gsrc,
+                                                       const T* __restrict__ bsrc, Slab32 s, Params<T> P,
+                                                       SParamsT<T> Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
                                                        double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
                                                        int ntasks) {
-  __shared__ __attribute__((aligned(16))) float sm[SMarch<KK>::SZ];
+  __shared__ __attribute__((aligned(16))) T sm[SMarch<KK>::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
   const bool stopped = stop_requested(ctrl, ro, flag);
@@ -432,9 +436,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
     if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
-      smarch_task<KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
     else
-      smarch_task<KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
   }
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {

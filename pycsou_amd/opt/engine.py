@@ -549,14 +549,16 @@ class PDS2DStencilEngine(PDS2DEngine):
             self.Gb = torch.empty(N, dtype=dtype, device=dev)
         gsrc = None if fk == L.PCS_F_NULL else (self.Gb if fk == L.PCS_F_GRADBUF else self.y)
         self.fkind = fk
-        # fp32 images the general-stencil row-marching kernel covers (pds_smarch.hpp: 64-column
-        # strips, 16-B groups) run through pcs_pds2d_step with K in the args; the rest through the
-        # tile kernel (pcs_pds2d_stencil_step).  PCS_STENCIL_MARCH=0: always the tile kernel.
+        # images the general-stencil row-marching kernel covers (pds_smarch.hpp: 64-column strips,
+        # 4-column groups; fp32 and fp64, every K kind in fp64) run through pcs_pds2d_step with K in
+        # the args; the rest through the tile kernel (pcs_pds2d_stencil_step).  PCS_STENCIL_MARCH=0:
+        # always the tile kernel.
         self.march = False
         a = None
-        if dtype == torch.float32 and os.environ.get('PCS_STENCIL_MARCH', '1') != '0':
+        f64 = dtype == torch.float64
+        if dtype in (torch.float32, torch.float64) and os.environ.get('PCS_STENCIL_MARCH', '1') != '0':
             a = L.PdsArgs()
-            a.dtype, a.fkind, a.hkind, a.gkind = L.PCS_F32, fk, spec['hkind'], spec['gkind']
+            a.dtype, a.fkind, a.hkind, a.gkind = L.PCS_F64 if f64 else L.PCS_F32, fk, spec['hkind'], spec['gkind']
             a.n0, a.n1, a.row0, a.rows = n0, n1, 0, n0
             a.kkind, a.edge = spec['kkind'], int(spec['edge'])
             a.w0, a.w1 = spec['weights']
@@ -572,7 +574,7 @@ class PDS2DStencilEngine(PDS2DEngine):
                 a.gbuf = gsrc.data_ptr()
                 # separable PSF: grad F = N x - Conv^T y (the in-plane normal-operator kernel into the
                 # gradient buffer, then the march step), Conv^T y formed once here in fp64
-                sep = self.conv.separable(rtol=2e-7)
+                sep = self.conv.separable(rtol=1e-13 if f64 else 2e-7)
                 if sep is not None and sep[2] <= 7:
                     t0, t1, half = sep
                     self.taps = [torch.as_tensor(t).to(device=dev, dtype=dtype) for t in (t0, t1)]
@@ -581,11 +583,14 @@ class PDS2DStencilEngine(PDS2DEngine):
                     a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
                     a.cty = self.cty.data_ptr()
                     # the N tables: backward / centred K take the fused normal-operator march (one
-                    # launch, pds_nmarch.hpp) when the library does -- supported with no gradient buffer
-                    self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
-                    a.ntaps = self.ntaps.data_ptr()
-                    a.gbuf = None
-                    self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+                    # launch, pds_nmarch.hpp, fp32) when the library does -- supported with no gradient
+                    # buffer; fp64 takes the two-launch form (N x by k_sep2d_nrm, then the march step)
+                    self.nm_fused = False
+                    if not f64:
+                        self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+                        a.ntaps = self.ntaps.data_ptr()
+                        a.gbuf = None
+                        self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
                     a.gbuf = gsrc.data_ptr()
                     if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
                         a.fkind, a.cty, a.ntaps = fk, None, None

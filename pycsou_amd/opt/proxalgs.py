@@ -290,6 +290,14 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         F = None if isinstance(self.F, NullDifferentiableFunctional) else self.F
         if self.engine_mode == 'stencil':  # the general-stencil fused step only (tests, benchmarks)
             return match_stencil2d(F, self.G, self.H, self.K, self._H)
+        K = self.K
+        if (self._compute_dtype() == torch.float64 and len(getattr(K, 'dims', ())) == 2 and K.dims[1] >= 128
+                and K.dims[1] % 4 == 0):
+            # fp64 (the reference's default dtype) on images the row march covers: every 2-D K kind on
+            # the general-stencil engine, whose march has an fp64 form (the forward-Gradient fp32
+            # kernels do not); narrower images keep the tile kernels
+            return (match_stencil2d(F, self.G, self.H, self.K, self._H) or match_pds2d(F, self.G, self.H, self.K, self._H)
+                    or match_pds3d(F, self.G, self.H, self.K, self._H))
         return (match_pds2d(F, self.G, self.H, self.K, self._H) or match_stencil2d(F, self.G, self.H, self.K, self._H)
                 or match_pds3d(F, self.G, self.H, self.K, self._H))
 

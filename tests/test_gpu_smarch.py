@@ -79,7 +79,7 @@ def _oracle(p):
     return x, z, d
 
 
-def _fused(p):
+def _fused(p, dtype=np.float32):
     from pycsou_amd.func.loss import SquaredL2Loss
     from pycsou_amd.func.penalty import L1Norm, L21Norm, NonNegativeOrthant, Segment
     from pycsou_amd.linop.conv import Convolve2D
@@ -89,7 +89,7 @@ def _fused(p):
     shape, N = p['shape'], p['N']
     F = None
     if p['fk'] != 'null':
-        F = (1 / 2) * SquaredL2Loss(dim=N, data=p['y'].astype(np.float32))
+        F = (1 / 2) * SquaredL2Loss(dim=N, data=p['y'].astype(dtype))
     if p['psf'] is not None:
         C = Convolve2D(N, p['psf'], shape)
         C.lipschitz_cst = C.diff_lipschitz_cst = 1.0
@@ -103,7 +103,7 @@ def _fused(p):
     K.lipschitz_cst = K.diff_lipschitz_cst = _lip(p)
     H = p['lam'] * (L21Norm(dim=Hdim, groups=np.tile(np.arange(N), 2)) if p['hname'] == 'l21' else L1Norm(dim=Hdim))
     G = {'nonneg': NonNegativeOrthant(N), 'segment': Segment(N, 0.0, 1.0)}.get(p['gname'], None)
-    pds = PDS(dim=N, F=F, G=G, H=H, K=K, x0=np.zeros(N, np.float32), z0=np.zeros(Hdim, np.float32),
+    pds = PDS(dim=N, F=F, G=G, H=H, K=K, x0=np.zeros(N, dtype), z0=np.zeros(Hdim, dtype),
               max_iter=NITER - 1, min_iter=NITER - 1, accuracy_threshold=0.0, verbose=None, engine='stencil')
     est, _, diag = pds.iterate()
     eng = pds._engine
@@ -189,3 +189,51 @@ def test_fused_normal_march_matches_two_launch(kind, monkeypatch):
     x0, z0, d0, e0 = _fused(p)
     assert e1.nm_fused and not e0.nm_fused
     assert rel(x1, x0) < 2e-6 and rel(z1, z0) < 2e-6, (rel(x1, x0), rel(z1, z0))
+
+
+@pytest.mark.parametrize('case', range(len(CASES)), ids=lambda i: f'f64-{CASES[i][1]}-{CASES[i][0][0]}x{CASES[i][0][1]}')
+def test_smarch_fp64_vs_oracle(case):
+    """The same cases in fp64 (the reference's default dtype: pycsou/opt/proxalgs.py:327,341,
+    linop/diff.py:777): the fp64 form of the row march for every K kind, the forward Gradient included,
+    and separable PSFs as N x by k_sep2d_nrm<double> + the march step.  Bar: x and z to 1e-10 relative,
+    both diagnostics columns to 1e-9 relative (fp64 against fp64: operation order only)."""
+    from pycsou_amd import _lib as L
+    shape, kind, hname, fk, gname, edge, steps, weights = CASES[case]
+    p = _problem(shape, kind, hname, fk, gname, edge, steps, weights, seed=case)
+    xr, zr, dr = _oracle(p)
+    x, z, diag, eng = _fused(p, np.float64)
+    assert eng.march, 'the fp64 row-marching kernel must take this problem'
+    assert eng.args.dtype == L.PCS_F64
+    if fk.startswith('sep'):
+        assert eng.fkind == L.PCS_F_SEPCONV and eng.cty is not None and not eng.nm_fused
+    assert x.dtype == np.float64
+    assert rel(x, xr) < 1e-10, rel(x, xr)
+    assert rel(z, zr) < 1e-10, rel(z, zr)
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:], dr['primal'][1:],
+                               rtol=1e-9)
+    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float)[1:], dr['dual'][1:],
+                               rtol=1e-9)
+
+
+def test_fp64_default_routing_takes_the_march():
+    """A reference-default fp64 script (NumPy float64 arrays, K = Gradient(shape) centred, and the forward
+    K) on a C3-shaped image strip goes to the fp64 march through engine='fused' (auto)."""
+    from pycsou_amd.func.loss import SquaredL2Loss
+    from pycsou_amd.func.penalty import L21Norm
+    from pycsou_amd.linop.conv import Convolve2D
+    from pycsou_amd.linop.diff import Gradient
+    from pycsou_amd.opt.engine import PDS2DStencilEngine
+    from pycsou_amd.opt.proxalgs import PDS
+    shape = (96, 512)
+    N = shape[0] * shape[1]
+    y = np.random.default_rng(0).uniform(0, 1, N)
+    for kind in ('centered', 'forward'):
+        C = Convolve2D(N, OR.gaussian_psf(15, 2.0), shape)
+        C.compute_lipschitz_cst()
+        K = Gradient(shape, kind=kind)
+        K.compute_lipschitz_cst()
+        pds = PDS(dim=N, F=(1 / 2) * SquaredL2Loss(dim=N, data=y) * C,
+                  H=0.05 * L21Norm(dim=2 * N, groups=np.tile(np.arange(N), 2)), K=K, max_iter=5, min_iter=5,
+                  accuracy_threshold=0.0, verbose=None)
+        pds.iterate()
+        assert isinstance(pds._engine, PDS2DStencilEngine) and pds._engine.march, kind
