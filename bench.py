@@ -319,11 +319,11 @@ def fused_2d(pds, dtype, K, W, chunk=32):
     """Exactly W untimed then K timed iterations of a fused 2-D problem (PDS2DEngine, fixed
     count); HIP events on the launch stream bracket the K iterations.  Returns ms per
     iteration, the isolated per-kernel launch means and the engine facts."""
-    from pycsou_amd.opt.engine import PDS2DEngine, PDS2DStencilEngine
+    from pycsou_amd import _ops as O
+    from pycsou_amd.opt.engine import engine_class
     spec = pds._fused_spec()
     assert spec is not None, 'problem must take the fused 2-D engine'
-    eng = (PDS2DStencilEngine if spec.get('stencil') else PDS2DEngine)(spec, dtype, pds.tau, pds.sigma, pds.rho,
-                                                                       pds.x0, pds.z0)
+    eng = engine_class(spec)(spec, dtype, pds.tau, pds.sigma, pds.rho, O.to_dev(pds.x0, dtype), O.to_dev(pds.z0, dtype))
     total = W + K + 4
     eng.prepare_fixed(max(total, 4000), chunk)
     spin_up_fixed(eng)
@@ -567,27 +567,13 @@ def leg_conv63(args, dtype, K, W):
             'direct_flop_equiv_tflops': round(2 * 63 * 63 * n * n / (res['forward'] * 1e-3) / 1e12, 1)}
 
 
-def _kernel_launches(fn):
-    """GPU kernels launched while fn() runs (torch.profiler's device activity), or None when the
-    profiler cannot see the device on this box."""
-    try:
-        from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CUDA]) as prof:
-            fn()
-            torch.cuda.synchronize()
-        evs = [e for e in prof.events() if str(getattr(e, 'device_type', '')).endswith('CUDA')]
-        return len(evs)
-    except Exception:  # noqa: BLE001 -- a diagnostics field
-        return None
-
-
 def leg_cps_inpaint(args, dtype, K, W):
-    """A problem the fused engines do not match, on the generic per-operator device path: the
-    reference notebook's TV-LAD inpainting (CPS, K = LinOpVStack(Masking, Gradient(forward)),
-    H = ProxFuncHStack(L1Loss, mu L1Norm), G = Segment) at 2048^2 -- one kernel per operator call,
-    stopping rule on the device (proxalgs._DeviceLoop).  it/s from the difference of a (W + K)- and
-    a W-iteration iterate() (setup cancels), launches per iteration from torch.profiler's device
-    activity over the same difference."""
+    """The reference notebook's TV-LAD inpainting (CPS, K = LinOpVStack(Masking 50 %, Gradient(forward)),
+    H = ProxFuncHStack(L1Loss, mu L1Norm), G = Segment) at 2048^2: ONE launch per iteration (the masked
+    block inside the general-stencil row march, PCS_M_L1LOSS: PDS2DMaskEngine), timed as every fused 2-D
+    leg (HIP events around the K back-to-back iterations after W warm-up ones, steady state).
+    Algorithmic bytes: read x, z_s (2N), y and z_m (m each); write x', z_s', z_m' -- the engine moves
+    9 N words (z_m and y expanded to the image)."""
     from pycsou_amd.func import L1Loss, L1Norm, ProxFuncHStack, Segment
     from pycsou_amd.linop import Gradient, LinOpVStack, Masking
     from pycsou_amd.opt import CPS
@@ -596,43 +582,37 @@ def leg_cps_inpaint(args, dtype, K, W):
     rng = np.random.default_rng(5)
     mask = rng.random(N) < 0.5
     img = phantom((n, n), 12, 5).ravel()
-    y = torch.from_numpy(img[mask].astype(np.float32 if dtype == torch.float32 else np.float64)).cuda()
+    npdt = np.float32 if dtype == torch.float32 else np.float64
+    t0 = time.perf_counter()
+    y = torch.from_numpy(img[mask].astype(npdt)).cuda()
+    m = int(mask.sum())
     Gop = Masking(size=N, sampling_bool=mask)
     Gop.lipschitz_cst = Gop.diff_lipschitz_cst = 1.0
     D = Gradient(shape=(n, n), kind='forward')
-    D.lipschitz_cst = D.diff_lipschitz_cst = np.sqrt(8.0)
+    D.compute_lipschitz_cst()
     Kop = LinOpVStack(Gop, D)
-    H = ProxFuncHStack(L1Loss(dim=int(mask.sum()), data=y), 0.1 * L1Norm(dim=2 * N))
-    x0 = torch.zeros(N, dtype=dtype, device='cuda')
-
-    def run(iters):
-        cps = CPS(dim=N, G=Segment(dim=N, a=0, b=1), H=H, K=Kop, x0=x0, max_iter=iters, min_iter=iters,
-                  accuracy_threshold=0.0, verbose=None)
-        cps.iterate()
-        assert cps.iter == iters + 1 or cps.iter == iters, cps.iter
-        return cps.iter
-
-    run(max(W, 2))  # warm caches / allocator
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    n_a = run(W)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    n_b = run(W + K)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    ms = ((t2 - t1) - (t1 - t0)) * 1e3 / max(1, n_b - n_a)
-    la, lb = _kernel_launches(lambda: run(4)), _kernel_launches(lambda: run(14))
-    launches = None if la is None or lb is None else round((lb - la) / 10.0, 1)
+    H = ProxFuncHStack(L1Loss(dim=m, data=y), 0.1 * L1Norm(dim=2 * N))
+    cps = CPS(dim=N, G=Segment(dim=N, a=0, b=1), H=H, K=Kop, x0=torch.zeros(N, dtype=dtype, device='cuda'),
+              z0=torch.zeros(m + 2 * N, dtype=dtype, device='cuda'), verbose=None)
+    setup = time.perf_counter() - t0
+    spec = cps._fused_spec()
+    assert spec is not None and 'mask' in spec, 'the inpainting problem must take the fused masked step'
+    r = fused_2d(cps, dtype, K, W)
+    del cps
     elem = 4 if dtype == torch.float32 else 8
-    m = int(mask.sum())
-    alg = (1 + 1 + 1 + 2 * (m + 2 * N) / N) * N * elem  # read x, y (masked), write x'; z (m + 2N) in and out
+    alg = int((1 + 2 + 1 + 2 * m / N + 2 + m / N) * N * elem)  # x, z_s, y(m), z_m(m) in; x', z_s', z_m' out
+    eng_bytes = 9 * N * elem
+    km = r['kernels_ms']['step']
     return {'workload': f'CPS TV-LAD inpainting {n}x{n} {args.dtype} (reference notebook problem): K = LinOpVStack('
                         f'Masking 50 %, Gradient(forward)), H = ProxFuncHStack(L1Loss, 0.1*L1Norm), G = Segment(0, 1); '
-                        f'generic per-operator device path (no fused match), stopping rule on the device',
-            'it_per_s': round(1e3 / ms, 1), 'ms_per_iter': round(ms, 5), 'steps': K, 'warmup': W,
-            'launches_per_iter': launches, 'alg_bytes_per_iter': int(alg),
-            'iteration_frac_of_hbm_peak': round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                        f'one launch per iteration (k_pds2d_smarch with the masked block, PDS2DMaskEngine)',
+            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5), 'steps': K,
+            'warmup': W, 'launches_per_iter': 1, 'alg_bytes_per_iter': alg, 'engine_bytes_per_iter': eng_bytes,
+            'setup_s': round(setup, 2),
+            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'roofline': {'bound': 'hbm', 'kernel': 'pcs_pds2d_step (k_pds2d_smarch<forward, MASK, L1>)',
+                         'kernel_ms': round(km, 5), 'achieved': round(alg / (km * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
 def slab_bench(n, dtype, K, W, world):

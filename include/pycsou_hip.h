@@ -285,7 +285,23 @@ typedef struct {
   const void* conv_adj;
   int conv_tier, pad3;
   void* rbuf;
+  /* ABI 6: a masked data-fidelity block (mkind PCS_M_L1LOSS), the reference notebook's TV-LAD
+   * inpainting solved by ChambollePockSplitting (pycsou/opt/proxalgs.py:628-716):
+   *   K = LinOpVStack(Masking(mask), K_s)  (linop/base.py:259-279, linop/sampling.py:125-196),
+   *   H = ProxFuncHStack(L1Loss(dim=m, data=y), lam * L1Norm | lam * L21Norm on K_s x)
+   *       (func/base.py:21-89, func/loss.py:222-268), K_s the kkind stencil above, F = 0 (fkind
+   *       PCS_F_NULL), whole images only (rows == n0), the general-stencil row march (n1 % 4 == 0,
+   *       at least two 64-column strips).
+   * The masked dual block z_m is held EXPANDED to the image: zm / zmn are n0*n1 arrays (0 where the
+   * mask is False, the sampled entries in image order elsewhere); ym is y expanded the same way
+   * with NaN where the mask is False.  z / zn hold the K_s block only.  pcs_pds2d_run swaps zm / zmn
+   * with x / xn.  The partials' z sums cover both blocks (= the reference's ||z|| over [z_m; z_s]). */
+  int mkind, pad4;
+  const void* ym;
+  const void* zm;
+  void* zmn;
 } pcs_pds2d_args;
+enum { PCS_M_NONE = 0, PCS_M_L1LOSS = 1 };
 /* 1 if pcs_pds2d_step runs these arguments (0: PCS_EUNSUPPORTED / invalid). */
 int pcs_pds2d_supported(const pcs_pds2d_args* a);
 int pcs_pds2d_ntaps_len(int half); /* 64 + 32 * tier(half); -1 beyond tier 7 */

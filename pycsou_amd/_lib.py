@@ -21,6 +21,7 @@ PCS_K_GRAD_FORWARD, PCS_K_GRAD_BACKWARD, PCS_K_GRAD_CENTERED, PCS_K_LAPLACIAN = 
 PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
 PCS_APGD_G_L1 = 3
 PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF, PCS_F_CONV2D, PCS_F_CONV0 = 0, 1, 2, 3, 4, 5
+PCS_M_NONE, PCS_M_L1LOSS = 0, 1
 KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
 
 _c_int, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -41,7 +42,8 @@ class PdsArgs(ctypes.Structure):
                 ('sums_out', _vp), ('pre_partials', _vp), ('n_pre', _c_i64),
                 ('cty', _vp), ('ntaps', _vp),
                 ('kkind', _c_int), ('edge', _c_int), ('w0', _c_dbl), ('w1', _c_dbl),
-                ('conv_fwd', _vp), ('conv_adj', _vp), ('conv_tier', _c_int), ('pad3', _c_int), ('rbuf', _vp)]
+                ('conv_fwd', _vp), ('conv_adj', _vp), ('conv_tier', _c_int), ('pad3', _c_int), ('rbuf', _vp),
+                ('mkind', _c_int), ('pad4', _c_int), ('ym', _vp), ('zm', _vp), ('zmn', _vp)]
 
 
 class StencilArgs(ctypes.Structure):
@@ -175,7 +177,7 @@ class HipError(ValueError):
 
 
 # the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 def load():

@@ -480,13 +480,15 @@ static bool use_march(const pcs_pds2d_args* a);
 // fp64 (the reference's default dtype): every K kind, the forward Gradient included, takes this march
 // (the forward-only fp32 kernels pds_pt.hpp / pds_nmarch.hpp have no fp64 form)
 static bool use_smarch(const pcs_pds2d_args* a) {
-  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward() && a->dtype != PCS_F64) return false;
+  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward() && a->dtype != PCS_F64 && a->mkind == PCS_M_NONE) return false;
   // separable PSF with backward / centred K: the fused normal-operator march (one launch) when it applies
   if (a->kkind != PCS_K_GRAD_FORWARD && a->fkind == PCS_F_SEPCONV && use_march(a)) return false;
   if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return false;
   if ((a->dtype != PCS_F32 && a->dtype != PCS_F64) || !make_slab(a).vec) return false;
   if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF &&
       !((a->kkind != PCS_K_GRAD_FORWARD || a->dtype == PCS_F64) && sm_normal(a)))
+    return false;
+  if (a->mkind != PCS_M_NONE && (a->fkind != PCS_F_NULL || !aligned16(a->ym) || !aligned16(a->zm) || !aligned16(a->zmn)))
     return false;
   if (a->hkind != PCS_H_L1 && (a->hkind != PCS_H_L21 || a->kkind == PCS_K_LAPLACIAN)) return false;
   const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
@@ -521,9 +523,12 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
                : (FK == PCS_F_GRADBUF || FK == SM_F_NB) ? (const T*)a->gbuf
                                                         : nullptr;
   const T* b = FK == SM_F_NB ? (const T*)a->cty : nullptr;
+  if constexpr (FK == SM_F_MASK) g = (const T*)a->ym;
+  const T* mi = FK == SM_F_MASK ? (const T*)a->zm : nullptr;
+  T* mo = FK == SM_F_MASK ? (T*)a->zmn : nullptr;
   k_pds2d_smarch<T, KK, FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
-      (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, s, P, make_sparams<T>(a), a->gkind, a->partials,
-      (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
+      (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, mi, mo, s, P, make_sparams<T>(a), a->gkind,
+      a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
   return launch_status();
 }
 
@@ -550,6 +555,7 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
     if (rc != PCS_OK) return rc;
     return launch_smarch<T, KK, SM_F_NB>(a, rb, st);
   }
+  if (a->mkind == PCS_M_L1LOSS) return launch_smarch<T, KK, SM_F_MASK>(a, rb, st);
   if (a->fkind == PCS_F_DENOISE) return launch_smarch<T, KK, PCS_F_DENOISE>(a, rb, st);
   if (a->fkind == PCS_F_GRADBUF) return launch_smarch<T, KK, PCS_F_GRADBUF>(a, rb, st);
   return launch_smarch<T, KK, PCS_F_NULL>(a, rb, st);
@@ -705,6 +711,10 @@ static int check_args(const pcs_pds2d_args* a) {
   if ((a->fkind == PCS_F_DENOISE || a->fkind == PCS_F_SEPCONV) && !a->y) return PCS_EINVAL;
   if (a->fkind == PCS_F_GRADBUF && !a->gbuf) return PCS_EINVAL;
   if (a->fkind == PCS_F_SEPCONV && (!a->taps0 || !a->taps1 || a->half < 0)) return PCS_EINVAL;
+  if (a->mkind != PCS_M_NONE) {  // the masked block: whole images, F = 0, the row march only
+    if (a->mkind != PCS_M_L1LOSS || a->fkind != PCS_F_NULL || multi || !a->ym || !a->zm || !a->zmn) return PCS_EINVAL;
+    if (!use_smarch(a)) return PCS_EUNSUPPORTED;
+  }
   const int hxn = needed_halo_x(a->fkind, a->half);
   if (hxn < 0) return PCS_EUNSUPPORTED;
   if (multi && (a->halo_x < hxn || a->halo_z < 1 ||
@@ -768,8 +778,10 @@ int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t st) {
   for (int64_t i = 0; i < n; ++i) {
     if (i % 2) {
       b.x = a->xn, b.xn = const_cast<void*>(a->x), b.z = a->zn, b.zn = const_cast<void*>(a->z);
+      b.zm = a->zmn, b.zmn = const_cast<void*>(a->zm);
     } else {
       b.x = a->x, b.xn = a->xn, b.z = a->z, b.zn = a->zn;
+      b.zm = a->zm, b.zmn = a->zmn;
     }
     const int rc = pcs_pds2d_step(&b, st);
     if (rc != PCS_OK) return rc;

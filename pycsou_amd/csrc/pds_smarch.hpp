@@ -62,8 +62,19 @@ namespace pcs {
 
 enum { SK_LAP = 3 };  // KK: PCS_FORWARD / PCS_BACKWARD / PCS_CENTERED (2 components) or the Laplacian (1)
 // FK beyond the public kinds: grad F = g - b with g = N x = Conv^T Conv x from a buffer (the in-plane
-// normal-operator kernel, pcs_conv2d_sep_ata_planes) and b = Conv^T y (formed once per problem)
-enum { SM_F_NB = 16 };
+// normal-operator kernel, pcs_conv2d_sep_ata_planes) and b = Conv^T y (formed once per problem);
+// SM_F_MASK: F = 0 and a masked data-fidelity block in K / H (below)
+enum { SM_F_NB = 16, SM_F_MASK = 32 };
+
+// SM_F_MASK: K = LinOpVStack(Masking, K_s), H = ProxFuncHStack(L1Loss(y), lam * L1 | L21) -- the reference
+// notebook's TV-LAD inpainting (pycsou/linop/base.py:159-279, func/base.py:21-89, func/loss.py:222-268,
+// solved by ChambollePockSplitting, opt/proxalgs.py:628-716).  The masked dual block z_m is held expanded
+// to the image (0 where the mask is False), y expanded with NaN where the mask is False (gsrc), so the
+// block is pointwise and lives in the U phase alone:
+//   K^T z = (0 + M^T z_m) + K_s^T z_s                        (LinOpStack.adjoint accumulation order)
+//   z_m'  = w - sigma ((prox_l1(w / sigma - y, 1 / sigma)) + y),  w = z_m + sigma u   (masked pixels)
+// (ProximableFunctional.fenchel_prox of the stack, core/functional.py:176-207, with the L1Loss prox
+// ProxFuncPreComp(L1Norm, 1, -y): prox_l1(v + (-y), tau) - (-y)).  msrc / mdst: z_m in / out.
 
 // the stencils on a 5-sample window: stencil.hpp (sw_d1_fwd / sw_d1_adj / sw_d2_fwd / sw_d2_adj)
 
@@ -107,6 +118,7 @@ template <typename T, int KK, int FK, int HK, bool CI>
 __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restrict__ xn,
                                             const T* __restrict__ z, T* __restrict__ zn,
                                             const T* __restrict__ gsrc, const T* __restrict__ bsrc,
+                                            const T* __restrict__ msrc, T* __restrict__ mdst,
                                             const Slab32& s, const Params<T>& P,
                                             const SParamsT<T>& Q, int gk, int s0, int s1, int c0, T* sm,
                                             double (&part)[4]) {
@@ -123,12 +135,14 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
   const int n0 = s.n0, n1 = s.n1, edge = Q.edge;
   const int zstride = (s.rows + 2 * s.hz) * n1;
   const View vx = make_view(x, s, s.hx, ES), vg = make_view(gsrc != nullptr ? gsrc : x, s, s.hy, ES),
-             vb = make_view(bsrc != nullptr ? bsrc : x, s, s.hy, ES);
+             vb = make_view(bsrc != nullptr ? bsrc : x, s, s.hy, ES),
+             vm = make_view(msrc != nullptr ? msrc : x, s, s.hx, ES);
   View vz[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) vz[d] = make_view(z + d * zstride, s, s.hz, ES);
   const uint32_t pitch = (uint32_t)n1 * ES;
   const Rsrc rxn = rsrc_of(xn, (uint32_t)(s.rows + 2 * s.hx) * pitch);
+  const Rsrc rmn = rsrc_of(mdst != nullptr ? mdst : xn, FK == SM_F_MASK ? (uint32_t)(s.rows + 2 * s.hx) * pitch : 0u);
   Rsrc rzn[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) rzn[d] = rsrc_of(zn + d * zstride, (uint32_t)zstride * ES);
@@ -163,11 +177,11 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
   }
   // x, y|g (and b) of the U items in two register sets: the set of step k + 1 loads at the top of
   // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index)
-  G4<T> zr[D][KZ], xr[2], gr[2], br[2];
+  G4<T> zr[D][KZ], xr[2], gr[2], br[2], mr[2];
 #if PCS_SM_ZEARLY
   G4<T> zr0[D][KZ];  // step 0's z rows, loaded with the prologue's (landed before the prologue's U)
 #endif
-  T xe[2] = {T(0), T(0)}, ge[2] = {T(0), T(0)}, be[2] = {T(0), T(0)};
+  T xe[2] = {T(0), T(0)}, ge[2] = {T(0), T(0)}, be[2] = {T(0), T(0)}, me[2] = {T(0), T(0)};
   // z rows [a + ZHI - 15, a + ZHI] (rows below rmin read as 0)
   auto loads_z_into = [&](G4<T>(&dst)[D][KZ], int a, int rmin) {
 #pragma unroll
@@ -195,7 +209,13 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
     const uint32_t ro = r < rmin ? kOOB : vx.row_off(r);
     xr[PB] = bload4t<T>(vx.r, ro + co_c);
     xe[PB] = bload1t<T>(vx.r, ro + co_e);
-    if constexpr (FK != PCS_F_NULL) {
+    if constexpr (FK == SM_F_MASK) {  // y (NaN = unmasked) on the own columns; z_m on both
+      const uint32_t rg = r < rmin ? kOOB : vg.row_off(r);
+      gr[PB] = bload4t<T>(vg.r, rg + co_c);
+      const uint32_t rm = r < rmin ? kOOB : vm.row_off(r);
+      mr[PB] = bload4t<T>(vm.r, rm + co_c);
+      me[PB] = bload1t<T>(vm.r, rm + co_e);
+    } else if constexpr (FK != PCS_F_NULL) {
       const uint32_t rg = r < rmin ? kOOB : vg.row_off(r);
       gr[PB] = bload4t<T>(vg.r, rg + co_c);
       ge[PB] = bload1t<T>(vg.r, rg + co_e);
@@ -236,8 +256,8 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
                       hc.v[2], hc.v[3], hr.v[0], hr.v[1], hr.v[2], hr.v[3]};
     const bool rrow = RI || (unsigned)gr_ < (unsigned)n0;
     const bool own = lr >= s0 && lr < s1 && rrow && cin;
-    G4<T> uo, xo;
-    T ue = T(0), sdx = T(0), sx = T(0);
+    G4<T> uo, xo, mo;
+    T ue = T(0), sdx = T(0), sx = T(0), sdm = T(0), sm2 = T(0);
 #pragma unroll
     for (int m = 0; m < 5; ++m) {
       const int i1 = m < 4 ? c + m : ce;
@@ -254,6 +274,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
         kt = pcs_fma(sw_d1_adj<KK, RI>(w0, gr_, n0, edge), P.inv_step0,
                     sw_d1_adj<KK, CI>(w1, i1, n1, edge) * P.inv_step1);
       }
+      if constexpr (FK == SM_F_MASK) kt = (m < 4 ? mr[PB].v[m] : me[PB]) + kt;  // (0 + M^T z_m) + K_s^T z_s
       const T xv = m < 4 ? xr[PB].v[m] : xe[PB];
       T gf = T(0);
       if constexpr (FK == PCS_F_DENOISE) gf = xv - (m < 4 ? gr[PB].v[m] : ge[PB]);  // (2 (x + (-y))) 0.5, exact
@@ -269,6 +290,18 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
         const T dx = xv - xnew;
         sdx += dx * dx;
         sx += xv * xv;
+        if constexpr (FK == SM_F_MASK) {  // the masked block's z_m', pointwise (K u = M u here)
+          const T yv = gr[PB].v[m], zmv = mr[PB].v[m];
+          const T w = zmv + P.sigma * u;
+          const T a = w * P.inv_sigma + (-yv);  // ProxFuncPreComp: v + (-y)
+          const T pl = a - P.inv_sigma * clip1(a * P.sigma);  // prox_l1(a, 1 / sigma)
+          const T zt = w - P.sigma * (pl - (-yv));
+          const T zo = (yv == yv) ? pcs_fma(P.rho, zt, P.omr * zmv) : T(0);  // NaN y: not sampled
+          mo.v[m] = zo;
+          const T dm = zmv - zo;
+          sdm += dm * dm;
+          sm2 += zmv * zmv;
+        }
       } else {
         ue = u;
       }
@@ -276,7 +309,12 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
     if (own) {
       part[0] += (double)sdx;
       part[1] += (double)sx;
+      if constexpr (FK == SM_F_MASK) {
+        part[2] += (double)sdm;
+        part[3] += (double)sm2;
+      }
     }
+    if constexpr (FK == SM_F_MASK) bstore4t<T, PCS_SM_SAUX>(rmn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, mo);
     T* urow = UR + (lr & 31) * WZ;
     st4(urow + lc, uo);
     if (ext_st) urow[lce] = ue;
@@ -415,7 +453,8 @@ template <typename T, int KK, int FK, int HK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE))) void k_pds2d_smarch(const T* __restrict__ x, T* __restrict__ xn,
                                                        const T* __restrict__ z, T* __restrict__ zn,
                                                        const T* __restrict__ gsrc,
-                                                       const T* __restrict__ bsrc, Slab32 s, Params<T> P,
+                                                       const T* __restrict__ bsrc, const T* __restrict__ msrc,
+                                                       T* __restrict__ mdst, Slab32 s, Params<T> P,
                                                        SParamsT<T> Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
                                                        double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
                                                        int ntasks) {
@@ -436,9 +475,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
     if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
-      smarch_task<T, KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part);
     else
-      smarch_task<T, KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part);
   }
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {

@@ -292,6 +292,11 @@ class PDS2DEngine:
         if self.persistent:
             self.bar = torch.zeros(int(self.lib.pcs_grid_bar_bytes()) // 4, dtype=torch.int32, device=dev)
 
+    def _bind(self, a, p):
+        """Point the step's iterate buffers at parity p (reads buffers p, writes 1 - p)."""
+        a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
+        a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+
     # the fused step / the chunk of n steps launched back to back from C, on self.args
     def _step_call(self, st):
         L.check(self.lib.pcs_pds2d_step(ctypes.byref(self.args), st), 'pcs_pds2d_step')
@@ -304,8 +309,7 @@ class PDS2DEngine:
         a, lib, st = self.args, self.lib, L.stream()
         if self.fkind == L.PCS_F_GRADBUF:
             self._grad_conv(p, st)
-        a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
-        a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        self._bind(a, p)
         a.hist = hist.data_ptr() if self.fused_finalize else None
         self._step_call(st)
         if not self.fused_finalize:
@@ -335,8 +339,7 @@ class PDS2DEngine:
 
     def _chunk_native(self, hist):
         a = self.args
-        a.x, a.xn = self.X[0].data_ptr(), self.X[1].data_ptr()
-        a.z, a.zn = self.Z[0].data_ptr(), self.Z[1].data_ptr()
+        self._bind(a, 0)
         a.hist = hist.data_ptr()
         if self.persistent:
             rc = self.lib.pcs_pds2d_run_persistent(ctypes.byref(a), self.chunk, L.ptr(self.bar), L.stream())
@@ -382,8 +385,7 @@ class PDS2DEngine:
         p = getattr(self, '_fixed_p', 0)
         if self.native:
             a = self.args
-            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
-            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            self._bind(a, p)
             a.hist = self.hist.data_ptr()
             self._run_call(int(n))
             self._fixed_p = p ^ (int(n) & 1)
@@ -431,8 +433,7 @@ class PDS2DEngine:
                 timed('conv_adj', lambda: L.check(lib.pcs_conv2d_planned(
                     a.dtype, L.ptr(self.R), L.ptr(self.Gb), n0, n1, L.ptr(adj[1]), adj[0], None, 0.0, L.stream()),
                     'pcs_conv2d_planned'))
-            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
-            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            self._bind(a, p)
             a.hist = self.hist.data_ptr()
             timed('step', lambda: self._step_call(L.stream()))
         torch.cuda.synchronize()
@@ -453,8 +454,7 @@ class PDS2DEngine:
             a.hist = None
         for i in range(n):
             p = i % 2
-            a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
-            a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+            self._bind(a, p)
             evs[i][0].record(st)
             self._step_call(L.stream())
             evs[i][1].record(st)
@@ -662,3 +662,121 @@ class PDS2DStencilEngine(PDS2DEngine):
         if self.march:
             return PDS2DEngine._run_call(self, n)
         L.check(self.lib.pcs_pds2d_stencil_run(ctypes.byref(self.args), int(n), L.stream()), 'pcs_pds2d_stencil_run')
+
+
+def match_masked_stencil2d(F, G, H, K, has_H):
+    """Engine spec for the masked data-fidelity problem of the reference notebook (TV-LAD inpainting,
+    solved by ChambollePockSplitting, pycsou/opt/proxalgs.py:628-716): F = 0,
+    K = LinOpVStack(Masking(mask), K_s) (pycsou/linop/base.py:259-279, linop/sampling.py:125-196),
+    H = ProxFuncHStack(L1Loss(dim=m, data=y), lam * L1Norm | lam * L21Norm) (func/base.py:21-89,
+    func/loss.py:222-268) with K_s / the second block any problem match_stencil2d takes with F = 0;
+    G = None / NonNegativeOrthant / Segment.  Only images the row march covers (n1 % 4 == 0, at
+    least two 64-column strips); None otherwise (the generic per-operator path runs it)."""
+    from ..core.functional import ProxFuncPreComp
+    from ..func.base import ProxFuncHStack
+    from ..linop.base import LinOpStack
+    from ..linop.sampling import Masking
+    if not has_H or not (F is None or isinstance(F, NullDifferentiableFunctional)):
+        return None
+    if not isinstance(K, LinOpStack) or K.axis != 0 or len(K.linops) != 2 or not isinstance(H, ProxFuncHStack) \
+            or len(H.proxfuncs) != 2:
+        return None
+    M, Ks = K.linops
+    h_loss, h_s = H.proxfuncs
+    if not isinstance(M, Masking) or not hasattr(M, 'sampling_bool'):
+        return None
+    if not (isinstance(h_loss, ProxFuncPreComp) and isinstance(h_loss.prox_func, L1Norm)
+            and isinstance(h_loss.scale, (int, float)) and h_loss.scale == 1 and not np.isscalar(h_loss.shift)):
+        return None
+    m = int(M.shape[0])
+    if h_loss.dim != m or O.numel(h_loss.shift) != m:
+        return None
+    spec = match_stencil2d(None, G, h_s, Ks, True)
+    if spec is None or spec['fkind'] != L.PCS_F_NULL:
+        return None
+    n0, n1 = spec['shape']
+    if M.shape[1] != n0 * n1 or n1 % 4 or n1 <= 64:
+        return None
+    spec['mask'] = M.sampling_bool
+    spec['mask_shift'] = h_loss.shift  # = -y
+    spec['m'] = m
+    return spec
+
+
+class PDS2DMaskEngine(PDS2DEngine):
+    """The masked data-fidelity problem (match_masked_stencil2d) on the general-stencil row march with
+    the masked block inside the step (pcs_pds2d_args.mkind = PCS_M_L1LOSS, pds_smarch.hpp SM_F_MASK):
+    one launch per iteration.  The masked dual block z_m is held expanded to the image (ZM, 0 where the
+    mask is False) and y expanded with NaN there; the solver's z = [z_m; z_s] is assembled on return."""
+
+    def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, chunk=32, use_graph=True):
+        self.lib = L.gpu()
+        self.spec = spec
+        self.dtype = dtype
+        n0, n1 = spec['shape']
+        self.N = N = n0 * n1
+        nc, m = spec['ncomp'], spec['m']
+        dev = x0.device
+        self.idx = torch.as_tensor(np.flatnonzero(spec['mask']).astype(np.int64)).to(dev)
+        z0 = z0.to(dtype)
+        self.X = [x0.to(dtype).clone(), torch.empty(N, dtype=dtype, device=dev)]
+        self.Z = [z0[m:].clone(), torch.empty(nc * N, dtype=dtype, device=dev)]
+        self.ZM = [torch.zeros(N, dtype=dtype, device=dev), torch.zeros(N, dtype=dtype, device=dev)]
+        self.ZM[0][self.idx] = z0[:m]
+        self.ym = torch.full((N,), float('nan'), dtype=dtype, device=dev)
+        self.ym[self.idx] = -O.to_dev(spec['mask_shift'], dtype)  # y = -shift, exactly
+        self.chunk = max(2, chunk + (chunk % 2))
+        self.use_graph = use_graph
+        self.fkind = L.PCS_F_NULL
+        a = L.PdsArgs()
+        a.dtype = L.PCS_F64 if dtype == torch.float64 else L.PCS_F32
+        a.fkind, a.hkind, a.gkind = L.PCS_F_NULL, spec['hkind'], spec['gkind']
+        a.n0, a.n1, a.row0, a.rows = n0, n1, 0, n0
+        a.kkind, a.edge = spec['kkind'], int(spec['edge'])
+        a.w0, a.w1 = spec['weights']
+        a.tau, a.sigma, a.rho, a.lam = float(tau), float(sigma), float(rho), spec['lam']
+        a.step0, a.step1 = spec['steps']
+        a.seg_a, a.seg_b = spec['seg']
+        a.mkind, a.ym = L.PCS_M_L1LOSS, self.ym.data_ptr()
+        self.args = a
+        self._bind(a, 0)
+        a.partials = a.x  # placeholder for the support query (never written)
+        if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
+            raise ValueError('masked data-fidelity problem not supported by the fused step')
+        self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
+        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+        a.partials = self.partials.data_ptr()
+        self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
+        a.ctrl = self.ctrl.data_ptr()
+        self.fused_finalize = True
+        self.ws = torch.zeros(int(self.lib.pcs_pds2d_ws_bytes(ctypes.byref(a))) // 8 + 2, dtype=torch.float64,
+                              device=dev)
+        a.ws = self.ws.data_ptr()
+        self.graph = None
+        self.hist = None
+        self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        self.native = self.N >= NATIVE_MIN_PIXELS
+        self.persistent = False
+        self.bar = None
+
+    def _bind(self, a, p):
+        PDS2DEngine._bind(self, a, p)
+        a.zm, a.zmn = self.ZM[p].data_ptr(), self.ZM[1 - p].data_ptr()
+
+    def z_full(self, p):
+        """The solver's dual variable [z_m; z_s] of buffer parity p (the reference layout)."""
+        return torch.cat([self.ZM[p][self.idx], self.Z[p]])
+
+    def run(self, max_iter, min_iter, accuracy_threshold, has_dual=True):
+        n, x, _, h = PDS2DEngine.run(self, max_iter, min_iter, accuracy_threshold, has_dual)
+        return n, x, self.z_full(n % 2), h
+
+
+def engine_class(spec):
+    """The engine class of a fused spec (proxalgs and bench.py build engines through this)."""
+    from .engine3d import PDS3DEngine
+    if spec.get('ndim', 2) == 3:
+        return PDS3DEngine
+    if 'mask' in spec:
+        return PDS2DMaskEngine
+    return PDS2DStencilEngine if spec.get('stencil') else PDS2DEngine

@@ -285,7 +285,7 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
     def _fused_spec(self):
         if self.engine_mode in (False, 'generic'):
             return None
-        from .engine import match_pds2d, match_stencil2d
+        from .engine import match_masked_stencil2d, match_pds2d, match_stencil2d
         from .engine3d import match_pds3d
         F = None if isinstance(self.F, NullDifferentiableFunctional) else self.F
         if self.engine_mode == 'stencil':  # the general-stencil fused step only (tests, benchmarks)
@@ -299,7 +299,8 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
             return (match_stencil2d(F, self.G, self.H, self.K, self._H) or match_pds2d(F, self.G, self.H, self.K, self._H)
                     or match_pds3d(F, self.G, self.H, self.K, self._H))
         return (match_pds2d(F, self.G, self.H, self.K, self._H) or match_stencil2d(F, self.G, self.H, self.K, self._H)
-                or match_pds3d(F, self.G, self.H, self.K, self._H))
+                or match_pds3d(F, self.G, self.H, self.K, self._H)
+                or match_masked_stencil2d(F, self.G, self.H, self.K, self._H))
 
     def iterate(self):
         spec = self._fused_spec()
@@ -307,12 +308,11 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
             if self.engine_mode in ('fused', 'stencil'):
                 raise ValueError('problem does not match the fused PDS engine')
             return self._iterate_generic()
-        from .engine import PDS2DEngine, PDS2DStencilEngine
-        from .engine3d import PDS3DEngine
+        from .engine import engine_class
         dtype = self._compute_dtype()
         x0 = O.to_dev(self.x0, dtype)
         z0 = O.to_dev(self.z0, dtype)
-        eng = PDS3DEngine if spec.get('ndim', 2) == 3 else PDS2DStencilEngine if spec.get('stencil') else PDS2DEngine
+        eng = engine_class(spec)
         self._engine = eng(spec, dtype, self.tau, self.sigma, self.rho, x0, z0)
         n, x, z, hist = self._engine.run(self.max_iter, self.min_iter, self.accuracy_threshold, has_dual=True)
         self.iter = n

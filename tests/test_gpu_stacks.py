@@ -10,6 +10,7 @@ relative with identical iteration counts.
 import numpy as np
 import pytest
 
+from oracle import pycsou_ref as OR
 from tests.cases import load, rel
 
 pytestmark = pytest.mark.gpu
@@ -168,3 +169,93 @@ def test_apgd_tikhonov_notebook():
     est, _, diag = apgd.iterate()
     assert apgd.iter == int(g['n_iter'])
     assert rel(est['iterand'], g['x']) < 1e-9
+
+
+def _inpaint_problem(shape, seed, dtype, kind='forward', hname='l1'):
+    from pycsou_amd.func import L1Loss, L1Norm, L21Norm, ProxFuncHStack, Segment
+    from pycsou_amd.linop import Gradient, LinOpVStack, Masking
+    rng = np.random.default_rng(seed)
+    n = int(np.prod(shape))
+    mask = rng.random(n) < 0.4
+    img = np.clip(OR.phantom(shape, seed=seed).ravel() + 0.05 * rng.standard_normal(n), 0, 1)
+    y = img[mask].astype(dtype)
+    Gop = Masking(size=n, sampling_bool=mask)
+    D = Gradient(shape=shape, kind=kind)
+    mu = 0.6
+    Hs = mu * (L21Norm(dim=2 * n, groups=np.tile(np.arange(n), 2)) if hname == 'l21' else L1Norm(dim=2 * n))
+    H = ProxFuncHStack(L1Loss(dim=int(mask.sum()), data=y), Hs)
+    K = LinOpVStack(Gop, D)
+    K.lipschitz_cst = K.diff_lipschitz_cst = float(np.sqrt(1.0 + 8.0))
+    return n, mask, y, mu, K, H, Segment(dim=n, a=0, b=1)
+
+
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+@pytest.mark.parametrize('shape,thr,kind,hname', [((130, 200), 0.0, 'forward', 'l1'), ((257, 388), 1e-3, 'forward', 'l1'),
+                                                  ((96, 132), 0.0, 'centered', 'l21')])
+def test_cps_inpainting_fused_vs_oracle(dtype, shape, thr, kind, hname):
+    """The notebook's CPS TV-LAD inpainting (K = [Masking; Gradient], H = L1Loss (+) mu L1Norm, G =
+    Segment) on images the row march covers: ONE launch per iteration (the masked block inside the
+    general-stencil march, PCS_M_L1LOSS) against the oracle -- fp64 to 1e-9, fp32 to 5e-5, the same
+    iteration count (a natural stop included), the dual variable in the reference's [z_m; z_s] layout."""
+    from oracle import pycsou_ref as O
+    from pycsou_amd.opt import CPS
+    from pycsou_amd.opt.engine import PDS2DMaskEngine
+    n, mask, y, mu, K, H, G = _inpaint_problem(shape, 3, dtype, kind, hname)
+    max_iter = 30
+    m = int(mask.sum())
+    cps = CPS(dim=n, G=G, H=H, K=K, x0=np.zeros(n, dtype), z0=np.zeros(m + 2 * n, dtype), max_iter=max_iter,
+              min_iter=5 if thr > 0 else max_iter, accuracy_threshold=thr, verbose=None)
+    est, _, diag = cps.iterate()
+    assert isinstance(cps._engine, PDS2DMaskEngine), 'the masked fused step must take this problem'
+    assert est['primal_variable'].dtype == dtype
+    # oracle (tests/cases.py oracle_cps_inpaint semantics; the reference's op sequence)
+    from oracle import pylops1 as P
+    D = P.Gradient(shape, sampling=1., edge=True, kind=kind)
+    m = int(mask.sum())
+    yd = y.astype(np.float64)
+
+    def Kf(x):
+        return np.concatenate([x[mask], D.matvec(x)])
+
+    def KT(z):
+        xa = np.zeros(n)
+        xa[mask] = z[:m]
+        return 0 + xa + D.rmatvec(z[m:])
+
+    if hname == 'l21':
+        hs = O.postcomp(lambda v, t: O.prox_l21_pixel(v, t, 2), mu)
+    else:
+        hs = O.postcomp(O.prox_l1, mu)
+
+    def hprox(v, t):
+        return np.concatenate([O.prox_l1(v[:m] + (-yd), t) - (-yd), hs(v[m:], t)])
+
+    xr, zr, dr = O.pds(lambda x: np.zeros_like(x), lambda v, t: O.proj_segment(v, 0.0, 1.0), Kf, KT,
+                       lambda w, s: O.fenchel_prox(hprox, w, s), cps.tau, cps.sigma, cps.rho, np.zeros(n),
+                       np.zeros(m + 2 * n), max_iter=max_iter, min_iter=5 if thr > 0 else max_iter,
+                       accuracy_threshold=thr)
+    tol = 1e-9 if dtype == np.float64 else 5e-5
+    assert cps.iter == len(dr['primal']), (cps.iter, len(dr['primal']))
+    assert est['dual_variable'].shape == (m + 2 * n,)
+    assert rel(est['primal_variable'], xr) < tol, rel(est['primal_variable'], xr)
+    assert rel(est['dual_variable'], zr) < tol, rel(est['dual_variable'], zr)
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:], dr['primal'][1:],
+                               rtol=1e-7 if dtype == np.float64 else 1e-3)
+    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float)[1:], dr['dual'][1:],
+                               rtol=1e-7 if dtype == np.float64 else 1e-3)
+
+
+def test_cps_inpainting_fused_vs_generic():
+    """The fused masked step against the generic per-operator path on the same fp64 problem:
+    iterates to 1e-12 (operation order only)."""
+    from pycsou_amd.opt import CPS
+    out = {}
+    for mode in ('fused', 'generic'):
+        n, mask, y, mu, K, H, G = _inpaint_problem((200, 256), 8, np.float64)
+        cps = CPS(dim=n, G=G, H=H, K=K, max_iter=19, min_iter=19, accuracy_threshold=0.0, verbose=None)
+        cps.engine_mode = mode
+        est, _, _ = cps.iterate()
+        assert (cps._engine is not None) == (mode == 'fused')
+        out[mode] = est
+    assert rel(out['fused']['primal_variable'], out['generic']['primal_variable']) < 1e-12
+    assert rel(out['fused']['dual_variable'], out['generic']['dual_variable']) < 1e-12
