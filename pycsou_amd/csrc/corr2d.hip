@@ -331,9 +331,10 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
 // with the tap pair (w[q][j], w[q-1][j]) (zero past either end) and the input x[r+q][c+j] broadcast
 // to both lanes (op_sel: any register, no pair moves).  Each lane's sequence of fmaf is the scalar
 // kernel's, in the same order (plus one fma with a zero tap at either end), so the sums match it.
-// The point: a wave64 v_fma_f32 issues every 2 cycles only with two waves alternating on the SIMD
+// The idea: a wave64 v_fma_f32 issues every 2 cycles only with two waves alternating on the SIMD
 // (4 alone), and the scalar kernel sits at 2 waves / SIMD (VALU ~53 % busy, PMC r3_prof_corr); one
-// v_pk_fma_f32 does two lanes' worth in the 4 cycles, so one wave keeps the SIMD's FP32 rate.
+// v_pk_fma_f32 does two lanes' worth in the 4 cycles, so one wave would keep the SIMD's FP32 rate.
+// Measured slower (use_pk below): opt-in diagnostics only.
 // Geometry: 256 threads = 32 row pairs x 8 chunks of 8 columns (a 64-column strip, 64-row blocks);
 // a b128 lane group (16 lanes) reads 2 row pairs x 8 chunks: rows 2 apart, so the ring stores row
 // slot s at s * PB + (s >> 1) * 16 -- the second row of the group then sits an odd number of 16-B
@@ -588,10 +589,13 @@ static int launch(const T* x, T* out, int64_t n0, int64_t n1, const T* w, int ws
   return launch_status();
 }
 
-// the fp32 packed kernel (k_corr2d_pk) unless PCS_CORR_PK=0 (read per call: A/B and tests)
+// the fp32 packed kernel (k_corr2d_pk) only with PCS_CORR_PK=1 (read per call: A/B and tests).  Measured
+// slower than the scalar kernel: 4096^2, k = 15: 0.116-0.119 against 0.108-0.109 ms; k = 31: 0.391-0.404
+// against 0.332-0.340 (3 alternating reps, profiles/r4_corr_pk_ab.txt) -- the FMA issue rate of the
+// scalar kernel is not what bounds it, and the packed form reads twice the tap words per input row
 static bool use_pk() {
   const char* e = getenv("PCS_CORR_PK");
-  return e == nullptr || atoi(e) != 0;
+  return e != nullptr && atoi(e) != 0;
 }
 
 template <int K, bool FLIP, bool VEC>

@@ -515,8 +515,11 @@ constexpr int k3gTW = 128, k3gNT = 512;
 template <typename T>
 constexpr int k3g_rows() { return sizeof(T) == 4 ? PCS_3DG_ROWS32 : 8; }
 
+#ifndef PCS_3DG_MINB  // workgroups per CU the register budget targets (diagnostics builds override)
+#define PCS_3DG_MINB 1
+#endif
 template <typename T, int KK, int FK, bool VEC>
-__global__ __launch_bounds__(k3gNT) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
+__global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
                                                      const T* __restrict__ z, T* __restrict__ zn,
                                                      const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk, int edge,
                                                      double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
