@@ -43,6 +43,12 @@ namespace pcs {
 #ifndef PCS_SM_SAUX
 #define PCS_SM_SAUX 16
 #endif
+// fp64: a 4-column group is two 16-B stores 16 B apart, so each store instruction covers every other
+// 16-B chunk of the wave's span; written through (sc1) those halves leave as partial lines -- PMC
+// WRITE_SIZE 2.0x the bytes (profiles/r4_prof_c3f64_*) -- so fp64 stores are plain (L2 merges the halves)
+#ifndef PCS_SM_SAUX64
+#define PCS_SM_SAUX64 0
+#endif
 
 // step 0's z rows loaded and landed with the prologue's (1) or at step 0's top (0).  Parity green both
 // ways; no measurable difference on the 2048^2 legs (profiles/r3_ck44_ze_ab.txt): kept at 0
@@ -123,6 +129,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
                                             const SParamsT<T>& Q, int gk, int s0, int s1, int c0, T* sm,
                                             double (&part)[4]) {
   constexpr uint32_t ES = sizeof(T);
+  constexpr int SAUX = sizeof(T) == 4 ? PCS_SM_SAUX : PCS_SM_SAUX64;
   using M = SMarch<KK>;
   constexpr int NT = 256, TS = M::TS, TW = M::TW, WZ = M::WZ, GZ = M::GZ, D = M::D, RING = M::RING;
   constexpr int KZ = cdiv(M::NZN, NT);
@@ -314,11 +321,11 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
         part[3] += (double)sm2;
       }
     }
-    if constexpr (FK == SM_F_MASK) bstore4t<T, PCS_SM_SAUX>(rmn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, mo);
+    if constexpr (FK == SM_F_MASK) bstore4t<T, SAUX>(rmn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, mo);
     T* urow = UR + (lr & 31) * WZ;
     st4(urow + lc, uo);
     if (ext_st) urow[lce] = ue;
-    bstore4t<T, PCS_SM_SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
+    bstore4t<T, SAUX>(rxn, (own ? (uint32_t)(lr + s.hx) * pitch : kOOB) + co_c, xo);
   };
 
   // ---- Z: z' on row lr = a + ui, columns c .. c + 3
@@ -387,7 +394,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
     }
     const uint32_t off = (own ? (uint32_t)(lr + s.hz) * pitch : kOOB) + co_c;
 #pragma unroll
-    for (int d = 0; d < D; ++d) bstore4t<T, PCS_SM_SAUX>(rzn[d], off, o[d]);
+    for (int d = 0; d < D; ++d) bstore4t<T, SAUX>(rzn[d], off, o[d]);
   };
 
   // prologue: u on rows [s0 - UPRO, s0] (a pseudo-step at a = s0 - TS whose loads skip the rows

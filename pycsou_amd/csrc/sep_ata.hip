@@ -340,12 +340,18 @@ static int ata_padb(int kb, int offb) {
 template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
   static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
-  static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8, WI = 4 * GI;
+  static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8;
+  // fp64 LDS bank layout: a 4-column group is 32 B, so the 16 lanes of a ds_read_b128 group span 512 B;
+  // the staged rows get an odd 16-B slot pitch (PH reads rows r, r + 1) and ring row pairs alternate a
+  // 16-B offset (PV reads rows r, r + 2): every b128 lane group then hits 16 distinct slots
+  // (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2, profiles/r4_prof_c3f64_*)
+  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, WI = 4 * GI + PAD;
+  static __device__ __forceinline__ int rrow(int slot) { return slot * TX + ((slot >> 1) & 1) * PAD; }
   static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
   static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
   static constexpr int NTAB = 288;  // a_v[0..29), a_h[32..61), E_v lo / hi, E_h lo / hi (7 x 8 each)
   static_assert(NPH % NT == 0, "whole PH items per thread");
-  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TX + NTAB); }
+  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TX + PAD + NTAB); }
 };
 template <typename T> struct NrmCfg;
 #ifndef PCS_NRM_CFG
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* stg = reinterpret_cast<T*>(smem_raw);  // RS x WI staged input rows
   T* ring = stg + RS * WI;                  // RING x TX rows of the horizontal pass
-  T* tab = ring + RING * TX;                // NTAB
+  T* tab = ring + RING * TX + G::PAD;       // NTAB
   const int tid = threadIdx.x;
   {
     __shared__ double hs[32];  // the two filters in fp64
@@ -501,8 +507,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
     __builtin_amdgcn_s_waitcnt((G::NST & 15) | ((G::NST >> 4) << 14) | (7 << 4) | (15 << 8));
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-      const int e = l * NT + tid;
-      if (e < G::NIN) stq(stg + 4 * e, q[l]);
+      const int e = l * NT + tid, rr = e / GI, gg = e - rr * GI;
+      if (e < G::NIN) stq(stg + rr * WI + 4 * gg, q[l]);
     }
     Cur nxt = cur;
     bool more = true;
@@ -565,7 +571,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
         Q4<T> o;
 #pragma unroll
         for (int m = 0; m < 4; ++m) o.v[m] = acc[4 * p + m];
-        stq(ring + slot * TX + 4 * (g + p), o);
+        stq(ring + G::rrow(slot) + 4 * (g + p), o);
       }
     }
     lds_barrier();
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
           if (c * CH + j < NV) {
             int slot = base + c * CH + j;
             slot = slot >= RING ? slot - RING : slot;
-            wc[j] = ldsq(rcol + slot * TX);
+            wc[j] = ldsq(rcol + G::rrow(slot));
           }
         }
       };
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
             const int jr = top ? i : i - (n1 - 7), row0 = top ? 0 : n1 - 7;
             const T* e = top ? evl : evh;
             for (int c = 0; c < 7; ++c) {
-              const Q4<T> w = ldsq(ring + ((row0 + c - cur.a + 14) % RING) * TX + 4 * vg);
+              const Q4<T> w = ldsq(ring + G::rrow((row0 + c - cur.a + 14) % RING) + 4 * vg);
               const T ec = e[8 * jr + c];
 #pragma unroll
               for (int m = 0; m < 4; ++m) acc[rr].v[m] -= ec * w.v[m];
