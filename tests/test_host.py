@@ -277,3 +277,55 @@ def test_sep2d_nrm_tables_equal_dense_normal_operator(k, off, n):
             N[j, cc] -= sum(c(i - j) * c(i - cc) for i in range(-7, 0))
             N[n - 7 + j, n - 7 + cc] -= sum(c(7 + ii - j) * c(7 + ii - cc) for ii in range(7))
     np.testing.assert_allclose(N, C.T @ C, atol=1e-12)
+
+
+def test_pds2d_masked_block_and_fp64_dispatch():
+    """ABI 6 masked data-fidelity block (mkind = PCS_M_L1LOSS, the CPS inpainting step) and the fp64
+    general-stencil march: host-side support queries only (fake device addresses, nothing launched).
+    The masked block needs F = 0, whole images, its three buffers and the row march's geometry; fp64
+    runs every K kind, the forward Gradient included, and separable PSFs only with N x's buffer."""
+    import ctypes
+    from pycsou_amd import _lib
+    lib = _lib.load()
+    assert ctypes.sizeof(_lib.PdsArgs) % 8 == 0
+    for dt in (_lib.PCS_F32, _lib.PCS_F64):
+        for kk in (_lib.PCS_K_GRAD_FORWARD, _lib.PCS_K_GRAD_CENTERED, _lib.PCS_K_LAPLACIAN):
+            a = _lib.PdsArgs()
+            a.dtype, a.fkind, a.gkind = dt, _lib.PCS_F_NULL, _lib.PCS_G_SEGMENT
+            a.hkind = _lib.PCS_H_L1 if kk == _lib.PCS_K_LAPLACIAN else _lib.PCS_H_L21
+            a.kkind, a.edge = kk, 1
+            a.n0 = a.rows = 256
+            a.n1 = 512
+            a.sigma = a.step0 = a.step1 = 1.0
+            a.seg_b = 1.0
+            for f in ('x', 'xn', 'z', 'zn', 'partials', 'ym', 'zm', 'zmn'):
+                setattr(a, f, 0x10000)
+            a.mkind = _lib.PCS_M_L1LOSS
+            assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1, (dt, kk)
+            assert lib.pcs_pds2d_nblocks(ctypes.byref(a)) > 0
+            a.zmn = None
+            assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0  # missing buffer
+            a.zmn = 0x10000
+            a.fkind, a.y = _lib.PCS_F_DENOISE, 0x10000
+            assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0  # F must be 0
+            a.fkind = _lib.PCS_F_NULL
+            a.row0, a.rows, a.halo_x, a.halo_y, a.halo_z = 64, 128, 4, 4, 4
+            assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0  # slabs: no
+            a.row0, a.rows = 0, 256
+            a.n1 = 60
+            assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 0  # one strip: no march
+    # fp64 separable PSF, forward K: the march with N x into gbuf (two launches); without gbuf the
+    # tile kernel keeps it
+    a = _lib.PdsArgs()
+    a.dtype, a.fkind, a.hkind, a.gkind = _lib.PCS_F64, _lib.PCS_F_SEPCONV, _lib.PCS_H_L21, _lib.PCS_G_NULL
+    a.kkind, a.half = _lib.PCS_K_GRAD_FORWARD, 7
+    a.n0 = a.rows = 256
+    a.n1 = 512
+    a.sigma = a.step0 = a.step1 = 1.0
+    for f in ('x', 'xn', 'z', 'zn', 'y', 'partials', 'taps0', 'taps1', 'cty'):
+        setattr(a, f, 0x10000)
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1  # tile kernel
+    nb_tile = lib.pcs_pds2d_nblocks(ctypes.byref(a))
+    a.gbuf = 0x20000
+    assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+    assert lib.pcs_pds2d_nblocks(ctypes.byref(a)) != nb_tile  # the march's task count
