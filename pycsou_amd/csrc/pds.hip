@@ -428,7 +428,24 @@ static bool sm_forward() {
   return e != nullptr && atoi(e) != 0;
 }
 
-template <typename T>
+// 16-row halves per step of the march (SMarch RS): 2 = 32-row steps (twice the loads in flight per
+// barrier, half the steps) for the fp32 Laplacian, whose single z component leaves the LDS for 64-row
+// rings at 3 workgroups / CU; PCS_SM_RS=1|2 (read once) forces either for every fp32 K (A/B)
+static int sm_rs(const pcs_pds2d_args* a) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("PCS_SM_RS");
+    env = e ? atoi(e) : 0;
+  }
+  if (a->dtype != PCS_F32) return 1;
+  if (env == 1 || env == 2) return env;
+  return a->kkind == PCS_K_LAPLACIAN ? 2 : 1;
+}
+
+// resident workgroups (<= 3 per CU: fewer, longer row segments, as the pt kernel), queried once per
+// kernel shape: RS = 1 takes the centred-K kernel's occupancy for every K (rings of the same size or
+// smaller), RS = 2 its own K's
+template <typename T, int KK, int RS>
 static int sm_slots() {
   static int slots = 0;
   if (slots == 0) {
@@ -436,22 +453,36 @@ static int sm_slots() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_smarch<T, PCS_CENTERED, PCS_F_DENOISE, PCS_H_L21>,
-                                                     256, 0) != hipSuccess ||
+    constexpr int QK = RS == 1 ? PCS_CENTERED : KK;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, k_pds2d_smarch<T, QK, PCS_F_DENOISE, QK == SK_LAP ? PCS_H_L1 : PCS_H_L21, RS>, 256, 0) != hipSuccess ||
         nb < 1)
       nb = sizeof(T) == 4 ? 3 : 2;
     (void)hipGetLastError();
-    slots = cus * (nb < 3 ? nb : 3);  // as the pt kernel: fewer, longer row segments
+    slots = cus * (nb < 3 ? nb : 3);
     const char* e = getenv("PCS_SM_SLOTS");  // diagnostics: grid-size sweep
     if (e && atoi(e) > 0) slots = atoi(e);
   }
   return slots;
 }
 
+static int sm_slots_for(const pcs_pds2d_args* a, int rs) {
+  if (a->dtype == PCS_F64) return sm_slots<double, PCS_CENTERED, 1>();
+  if (rs == 1) return sm_slots<float, PCS_CENTERED, 1>();
+  switch (a->kkind) {
+    case PCS_K_GRAD_FORWARD: return sm_slots<float, PCS_FORWARD, 2>();
+    case PCS_K_GRAD_BACKWARD: return sm_slots<float, PCS_BACKWARD, 2>();
+    case PCS_K_LAPLACIAN: return sm_slots<float, SK_LAP, 2>();
+    default: return sm_slots<float, PCS_CENTERED, 2>();
+  }
+}
+
 static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tiles_x = (int)((a->n1 + 63) / 64);
   if (tiles_x < 2) return false;
-  plan_bands(rb, 16, tiles_x, a->dtype == PCS_F64 ? sm_slots<double>() : sm_slots<float>(), 4, p);
+  const int rs = sm_rs(a);
+  // at least 4 16-row halves per segment (2 steps of 32 rows)
+  plan_bands(rb, 16 * rs, tiles_x, sm_slots_for(a, rs), 4 / rs, p);
   return true;
 }
 
@@ -526,9 +557,12 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   if constexpr (FK == SM_F_MASK) g = (const T*)a->ym;
   const T* mi = FK == SM_F_MASK ? (const T*)a->zm : nullptr;
   T* mo = FK == SM_F_MASK ? (T*)a->zmn : nullptr;
-  k_pds2d_smarch<T, KK, FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
-      (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, mi, mo, s, P, make_sparams<T>(a), a->gkind,
-      a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
+  auto* kern = k_pds2d_smarch<T, KK, FK, HK, 1>;
+  if constexpr (sizeof(T) == 4)
+    if (sm_rs(a) == 2) kern = k_pds2d_smarch<T, KK, FK, HK, 2>;
+  kern<<<(unsigned)p.ntasks, 256, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, mi, mo, s, P,
+                                           make_sparams<T>(a), a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws,
+                                           red_out(a), p.tiles_x, p.bd, p.ntasks);
   return launch_status();
 }
 

@@ -22,6 +22,7 @@
 // h'[14 - t] with offset 14 - o.  Persistent grid, tasks (plane, row segment, strip) with the
 // strip fastest and an XCD-aware task map, as k_sep2d_march.
 #include <cstring>
+#include <type_traits>
 
 #include "vecio.hpp"
 
@@ -337,21 +338,26 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_CH  // PV window rows per pipelined chunk (0: 4); diagnostics
 #define PCS_NRM_CH 0
 #endif
+#ifndef PCS_NRM_PF2  // staged rows loaded two steps ahead (two register sets); diagnostics
+#define PCS_NRM_PF2 0
+#endif
 template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
   static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
   static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8;
   // fp64 LDS bank layout: a 4-column group is 32 B, so the 16 lanes of a ds_read_b128 group span 512 B;
-  // the staged rows get an odd 16-B slot pitch (PH reads rows r, r + 1) and ring row pairs alternate a
-  // 16-B offset (PV reads rows r, r + 2): every b128 lane group then hits 16 distinct slots
-  // (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2, profiles/r4_prof_c3f64_*)
-  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, WI = 4 * GI + PAD;
-  static __device__ __forceinline__ int rrow(int slot) { return slot * TX + ((slot >> 1) & 1) * PAD; }
+  // the staged rows get an odd 16-B slot pitch (PH reads rows r, r + 1 in one lane group) and the ring
+  // rows a pitch of TX + PAD with row pairs alternating a 16-B offset inside it (PV reads rows r, r + 2:
+  // 2 (TX + PAD) +- PAD elements apart = an odd number of 16-B slots mod 256 B): every b128 lane group
+  // then hits 16 distinct slots (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2,
+  // profiles/r4_prof_c3f64_*).  A row never reaches the next one's first element.
+  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, WI = 4 * GI + PAD, TP = TX + PAD;
+  static __device__ __forceinline__ int rrow(int slot) { return slot * TP + ((slot >> 1) & 1) * PAD; }
   static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
   static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
   static constexpr int NTAB = 288;  // a_v[0..29), a_h[32..61), E_v lo / hi, E_h lo / hi (7 x 8 each)
   static_assert(NPH % NT == 0, "whole PH items per thread");
-  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TX + PAD + NTAB); }
+  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TP + NTAB); }
 };
 template <typename T> struct NrmCfg;
 #ifndef PCS_NRM_CFG
@@ -411,8 +417,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
                 NL = G::NL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* stg = reinterpret_cast<T*>(smem_raw);  // RS x WI staged input rows
-  T* ring = stg + RS * WI;                  // RING x TX rows of the horizontal pass
-  T* tab = ring + RING * TX + G::PAD;       // NTAB
+  T* ring = stg + RS * WI;                  // RING rows (pitch TP, G::rrow) of the horizontal pass
+  T* tab = ring + RING * G::TP;             // NTAB
   const int tid = threadIdx.x;
   {
     __shared__ double hs[32];  // the two filters in fp64
@@ -481,9 +487,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
     c.ns = (c.b - c.a + 28 + RS - 1) / RS;
     return c;
   };
-  Q4<T> q[NL];
   // staged rows of step s: input rows a - 14 + s RS + rr, columns c0 - 16 + 4 gg (0 outside)
-  auto prefetch = [&](const Cur& c) {
+  auto prefetch = [&](const Cur& c, Q4<T>(&q)[NL]) {
     const T* src = in + c.plane * (int64_t)n1 * n2;
     const int kmax = c.b - c.a + 27;  // last staged row any output of [a, b) reads
     const int gc0 = c.strip * TX - 16;
@@ -498,34 +503,41 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
     }
   };
-  Cur cur = task_at(t0);
-  prefetch(cur);
-  const int vi = tid / GX, vg = tid - vi * GX;  // PV item: rows RB vi .. + RB - 1 of the step, group vg
-  for (;;) {
-    // the staged rows have landed; the previous step's RB row stores (4 / 8 dwordx4) may still
-    // be in flight (vector memory ops retire in order)
-    __builtin_amdgcn_s_waitcnt((G::NST & 15) | ((G::NST >> 4) << 14) | (7 << 4) | (15 << 8));
+  // the step after c (more = false: none; c itself is returned)
+  auto advance = [&](const Cur& c, bool& more) {
+    Cur n = c;
+    more = true;
+    if (c.s + 1 < c.ns) {
+      n.s = c.s + 1;
+    } else {
+      more = c.t + t_stride < t_end;
+      if (more) n = task_at(c.t + t_stride);
+    }
+    return n;
+  };
+  // the staged rows have landed (WAITN: the memory ops issued after them that may stay in flight --
+  // vector memory ops retire in order); rows -> LDS
+  auto stage = [&](const Q4<T>(&q)[NL], auto waitn) {
+    constexpr int WN = decltype(waitn)::value;
+    __builtin_amdgcn_s_waitcnt((WN & 15) | ((WN >> 4) << 14) | (7 << 4) | (15 << 8));
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       const int e = l * NT + tid, rr = e / GI, gg = e - rr * GI;
       if (e < G::NIN) stq(stg + rr * WI + 4 * gg, q[l]);
     }
-    Cur nxt = cur;
-    bool more = true;
-    if (cur.s + 1 < cur.ns) {
-      nxt.s = cur.s + 1;
-    } else {
-      more = cur.t + t_stride < t_end;
-      if (more) nxt = task_at(cur.t + t_stride);
-    }
+  };
+  auto issue = [&](const Cur& c, Q4<T>(&q)[NL]) {
 #if PCS_NRM_PRIO
     __builtin_amdgcn_s_setprio(3);
 #endif
-    prefetch(nxt);  // unconditional (the last step re-reads its own rows): the wait for these
-                    // loads at the next step then leaves this step's stores in flight
+    prefetch(c, q);
 #if PCS_NRM_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
+  };
+  // one step on the staged rows of cur: PH into the ring, PV from it -> HBM
+  auto body = [&](const Cur cur) {
+    const int vi = tid / GX, vg = tid - vi * GX;  // PV item: rows RB vi .. + RB - 1 of the step, group vg
     const int c0 = cur.strip * TX;
     const int sb = (cur.s * RS) % RING;  // ring slot of the step's first staged row
     lds_barrier();
@@ -647,9 +659,58 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
         nrm_bstore(dst, live && !(PCS_NRM_ABL & 1) ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB, acc[rr]);
       }
     }
+  };
+#if PCS_NRM_PF2
+  // two register sets, the rows of step k + 2 issued at step k's top: at a step's top its own loads,
+  // the previous two steps' stores and the next step's loads are in flight
+  Q4<T> qa[NL], qb[NL];
+  using W2 = std::integral_constant<int, NL + 2 * G::NST>;
+  Cur c0 = task_at(t0);
+  bool m1, m2, m3;
+  Cur c1 = advance(c0, m1);
+  prefetch(c0, qa);
+  prefetch(c1, qb);  // unconditional (re-reads c0's rows when there is no next step)
+  for (;;) {
+    stage(qa, W2{});
+    Cur c2 = c1;
+    m2 = false;
+    if (m1) c2 = advance(c1, m2);
+    issue(c2, qa);
+    body(c0);
+    if (!m1) break;
+    stage(qb, W2{});
+    Cur c3 = c2;
+    m3 = false;
+    if (m2) c3 = advance(c2, m3);
+    issue(c3, qb);
+    body(c1);
+    if (!m2) break;
+    c0 = c2;
+    c1 = c3;
+    m1 = m3;
+  }
+#else
+  Q4<T> q[NL];
+  Cur cur = task_at(t0);
+  prefetch(cur, q);
+  for (;;) {
+    // the previous step's RB row stores (4 / 8 dwordx4) may still be in flight
+    stage(q, std::integral_constant<int, G::NST>{});
+    Cur nxt = cur;
+    bool more = true;
+    if (cur.s + 1 < cur.ns) {
+      nxt.s = cur.s + 1;
+    } else {
+      more = cur.t + t_stride < t_end;
+      if (more) nxt = task_at(cur.t + t_stride);
+    }
+    issue(nxt, q);  // unconditional (the last step re-reads its own rows): the wait for these
+                    // loads at the next step then leaves this step's stores in flight
+    body(cur);
     if (!more) break;
     cur = nxt;
   }
+#endif
 }
 
 template <typename T>
