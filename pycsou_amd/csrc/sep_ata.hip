@@ -341,6 +341,9 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_PF2  // staged rows loaded two steps ahead (two register sets); diagnostics
 #define PCS_NRM_PF2 0
 #endif
+#ifndef PCS_NRM_PK  // fp32 PV taps as v_pk_fma_f32 on column pairs (tap broadcast); diagnostics
+#define PCS_NRM_PK 0
+#endif
 template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
   static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
@@ -398,6 +401,26 @@ __device__ __forceinline__ void nrm_bstore(Rsrc r, uint32_t off, const Q4<T>& a)
     u4 d;
     __builtin_memcpy(&d, a.v + h * VN, 16);
     __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(off + 16 * h), 0, 0);
+  }
+}
+
+// a += h w on 4 columns: two packed FMAs in fp32 (PCS_NRM_PK), four scalar ones otherwise
+template <typename T>
+__device__ __forceinline__ void nrm_fma4(Q4<T>& a, T h, const Q4<T>& w) {
+  if constexpr (sizeof(T) == 4 && PCS_NRM_PK) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v hh = {h, h};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      f2v ap = {a.v[2 * p], a.v[2 * p + 1]};
+      const f2v wp = {w.v[2 * p], w.v[2 * p + 1]};
+      ap = __builtin_elementwise_fma(hh, wp, ap);
+      a.v[2 * p] = ap.x;
+      a.v[2 * p + 1] = ap.y;
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a.v[m] += h * w.v[m];
   }
 }
 
@@ -624,9 +647,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
             for (int rr = 0; rr < RB; ++rr) {
               const int qq = v - rr;
               if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 4) || qq == 14)) {
-                const T h = av[qq < 14 ? 14 - qq : qq - 14];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) acc[rr].v[m] += h * w[c & 1][j].v[m];
+                nrm_fma4(acc[rr], av[qq < 14 ? 14 - qq : qq - 14], w[c & 1][j]);
               }
             }
           }
