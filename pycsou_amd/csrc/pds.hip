@@ -429,8 +429,11 @@ static bool sm_forward() {
 }
 
 // 16-row halves per step of the march (SMarch RS): 2 = 32-row steps (twice the loads in flight per
-// barrier, half the steps) for the fp32 Laplacian, whose single z component leaves the LDS for 64-row
-// rings at 3 workgroups / CU; PCS_SM_RS=1|2 (read once) forces either for every fp32 K (A/B)
+// barrier, half the steps; the Laplacian's single z component leaves the LDS for 64-row rings at 3
+// workgroups / CU).  Measured (tools/sm_probe.py, profiles/r4_sm_rs_ab.txt): Laplacian 2048^2 28.7 us
+// either way, 4096^2 82.0 against 76.6 us; centred 31.0 against 29.6-29.9 us at 2048^2 -- the 2048^2
+// time is not the per-step latency.  Default 1; PCS_SM_RS=2 (read once) for every fp32 K (parity
+// green at RS = 2 for every smarch case, profiles/r4_sm_rs_ab.txt)
 static int sm_rs(const pcs_pds2d_args* a) {
   static int env = -1;
   if (env < 0) {
@@ -438,8 +441,7 @@ static int sm_rs(const pcs_pds2d_args* a) {
     env = e ? atoi(e) : 0;
   }
   if (a->dtype != PCS_F32) return 1;
-  if (env == 1 || env == 2) return env;
-  return a->kkind == PCS_K_LAPLACIAN ? 2 : 1;
+  return env == 2 ? 2 : 1;
 }
 
 // resident workgroups (<= 3 per CU: fewer, longer row segments, as the pt kernel), queried once per

@@ -26,8 +26,12 @@ def med_ms(fn, n=10):
 
 def main():
     lib = L.load()
-    for n, dt in ((512, torch.float32), (1024, torch.float64)):
-        x = torch.randn(n, n, n, dtype=dt, device='cuda')
+    # PCS_ATA_CASES: comma list of NP:N:dtype (NP planes of N x N), default the C4 and C5 volumes
+    cases = os.environ.get('PCS_ATA_CASES', '512:512:f32,1024:1024:f64')
+    for c in cases.split(','):
+        npl, n, d = c.split(':')
+        npl, n, dt = int(npl), int(n), torch.float64 if d == 'f64' else torch.float32
+        x = torch.randn(npl, n, n, dtype=dt, device='cuda')
         t, g = torch.empty_like(x), torch.empty_like(x)
         r = np.arange(15) - 7.0
         h = np.exp(-0.5 * (r / 2.0) ** 2)
@@ -37,20 +41,20 @@ def main():
         code, st = L.dtcode(x), L.stream()
 
         def two():
-            assert lib.pcs_conv2d_sep_planes(code, L.ptr(x), L.ptr(t), n, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7, 0,
-                                             st) == 0
-            assert lib.pcs_conv2d_sep_planes(code, L.ptr(t), L.ptr(g), n, n, n, L.ptr(hf), 15, 7, L.ptr(hf), 15, 7, 0,
-                                             st) == 0
+            assert lib.pcs_conv2d_sep_planes(code, L.ptr(x), L.ptr(t), npl, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7,
+                                             0, st) == 0
+            assert lib.pcs_conv2d_sep_planes(code, L.ptr(t), L.ptr(g), npl, n, n, L.ptr(hf), 15, 7, L.ptr(hf), 15, 7,
+                                             0, st) == 0
 
         def one():
-            assert lib.pcs_conv2d_sep_ata_planes(code, L.ptr(x), L.ptr(t), n, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15, 7,
-                                                 st) == 0
+            assert lib.pcs_conv2d_sep_ata_planes(code, L.ptr(x), L.ptr(t), npl, n, n, L.ptr(hd), 15, 7, L.ptr(hd), 15,
+                                                 7, st) == 0
         t2 = med_ms(two)
-        for kern in ('2pass', '4pass'):  # k_sep2d_nrm (two 29-tap passes) / k_sep2d_ata (four 15-tap)
+        for kern in os.environ.get('PCS_ATA_KERNELS', '2pass,4pass').split(','):  # k_sep2d_nrm (two 29-tap passes) / k_sep2d_ata (four 15-tap)
             os.environ['PCS_ATA_KERNEL'] = kern
             t1 = med_ms(one)
             d = (g - t).abs().max().item() / g.abs().max().item()
-            print(f'{os.environ.get("PCS_LIB_PATH", "default")} n={n} {dt}: two passes {t2:.3f} ms, ata[{kern}] '
+            print(f'{os.environ.get("PCS_LIB_PATH", "default")} {npl}x{n}x{n} {dt}: two passes {t2:.3f} ms, ata[{kern}] '
                   f'{t1:.3f} ms, max rel diff {d:.2e}', flush=True)
         os.environ.pop('PCS_ATA_KERNEL')
         del x, t, g
