@@ -363,13 +363,16 @@ struct NrmG {
   static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TP + NTAB); }
 };
 template <typename T> struct NrmCfg;
+// 8-output PH items (PQ 2) since round 4: 512^3 fp32 0.483 against 0.495-0.500 ms, 1024^3 fp64 5.32-5.34
+// against 5.52-5.57 ms, 4096^2 fp64 0.105-0.107 against 0.108-0.109 ms (profiles/r4_nrm_var_ab.txt);
+// PCS_NRM_CFG=0 (diagnostics) the 4-output items
 #ifndef PCS_NRM_CFG
-#define PCS_NRM_CFG 0
+#define PCS_NRM_CFG 2
 #endif
 #if PCS_NRM_CFG == 0
 template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 1>; };
 template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 1>; };
-#elif PCS_NRM_CFG == 2  // diagnostics: 256 threads, 8-output PH items
+#elif PCS_NRM_CFG == 2  // 256 threads, 8-output PH items
 template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
 template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
 #else  // diagnostics: 128 threads, RB 8 / 4 and 16 / 8-output PH items -- fewer LDS bytes per
@@ -781,22 +784,26 @@ static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2
   if (np == 0) return PCS_OK;
   const int64_t nstrips = (n2 + G::TX - 1) / G::TX, pieces = np * nstrips;
   const int64_t slots = nrm_slots<T>();
-  // row segments: the count minimising (waves of resident workgroups) x (rows per task + the
-  // 28-row prologue), segments of >= 64 rows
+  // row segments: the fewest (each task re-reads a 28-row prologue) whose tasks fill the resident
+  // workgroup slots once, segments of >= 64 rows; then one task per workgroup, later workgroups
+  // starting as earlier ones finish.  Against the resident grid (a contiguous run of tasks per
+  // workgroup, segments by a waves x rows cost): 512^3 fp32 0.49 against 0.57-0.58 ms, 1024^3 fp64
+  // 5.96 (4 tasks per workgroup) against 7.33-7.44 ms, 4096^2 fp64 0.113 either way
+  // (profiles/r4_nrm_slots_sweep*.txt).  PCS_NRM_GRIDX=k (diagnostics): k x the resident slots, each
+  // workgroup a contiguous run of tasks
   const int64_t max_seg = n1 / 64 > 1 ? n1 / 64 : 1;
-  int64_t nseg = 1, best = -1;
-  for (int64_t c = 1; c <= max_seg; ++c) {
-    const int64_t len = (n1 + c - 1) / c, waves = (pieces * c + slots - 1) / slots;
-    const int64_t cost = waves * (len + 28);
-    if (best < 0 || cost < best) {
-      best = cost;
-      nseg = c;
-    }
-  }
+  int64_t nseg = 1;
+  while (nseg < max_seg && pieces * nseg < slots) ++nseg;
   const int64_t seg_len = (n1 + nseg - 1) / nseg;
   nseg = (n1 + seg_len - 1) / seg_len;
   const int64_t ntasks = pieces * nseg;
-  const int64_t grid = ntasks < slots ? ntasks : slots;
+  static int gridx = -1;
+  if (gridx < 0) {
+    const char* e = getenv("PCS_NRM_GRIDX");
+    gridx = e && atoi(e) > 0 ? atoi(e) : 0;
+  }
+  const int64_t gslots = gridx > 0 ? slots * gridx : ntasks;
+  const int64_t grid = ntasks < gslots ? ntasks : gslots;
   nrm_attr<T>();
   k_sep2d_nrm<T><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>((const T*)in, (T*)out, (int)n1, (int)n2,
                                                                 (int)nstrips, (int)nseg, (int)seg_len, ntasks,

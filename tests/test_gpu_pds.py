@@ -264,7 +264,7 @@ def test_pds3d_fused_matches_reference(name, dtype):
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 def test_pds3d_ata_opt_in_matches_reference(monkeypatch, dtype):
-    """The two-pass gradient (PCS_3D_ATA=1, the fp32 default: pcs_conv2d_sep_ata_planes + the
+    """The two-pass gradient (PCS_3D_ATA=1, the default: pcs_conv2d_sep_ata_planes + the
     axis-0 pass against C12^T y).  The golden volume's last axis (22) is not a multiple of 4,
     which the in-plane kernels need: there the engine keeps the three-pass chain (same
     trajectory); on a 24 x 20 x 24 volume the two-pass gradient runs and matches the oracle."""
@@ -415,8 +415,8 @@ def test_pds3d_ragged_tiles_vs_oracle(shape, dtype):
 @pytest.mark.parametrize('ata', ['', '0'])
 def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
     """Which 3-D gradient runs: by default the two-pass one (C12^T C12, then the axis-0 pass) for
-    fp32 and the three-pass chain for fp64; PCS_3D_ATA=0 pins the three-pass chain.  Either way
-    the iterates match the oracle."""
+    fp32 and fp64 (since round 4); PCS_3D_ATA=0 pins the three-pass chain.  Either way the iterates
+    match the oracle."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     if ata:
         monkeypatch.setenv('PCS_3D_ATA', ata)
@@ -427,7 +427,7 @@ def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
     c['tau'], c['sigma'], c['rho'] = pds.tau, pds.sigma, pds.rho
     est, _, _ = pds.iterate()
     assert isinstance(pds._engine, PDS3DEngine)
-    assert pds._engine.ata == (dtype == np.float32 and not ata)
+    assert pds._engine.ata == (not ata)
     x_ref, z_ref, _ = oracle_pds(c)
     tol = 1e-10 if dtype == np.float64 else 5e-5
     assert rel(est['primal_variable'], x_ref) < tol
