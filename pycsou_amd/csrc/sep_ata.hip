@@ -344,6 +344,42 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_PK  // fp32 PV taps as v_pk_fma_f32 on column pairs (tap broadcast); diagnostics
 #define PCS_NRM_PK 0
 #endif
+#ifndef PCS_NRM_SWZ  // lane-rotated 16-B chunk order of the LDS writes (below); diagnostics builds set 0
+#define PCS_NRM_SWZ 1
+#endif
+
+// NC consecutive 16-B chunks v (chunk j at p + j 16 B) written in the lane's order k -> chunk k ^ xm: the 8
+// lanes of a ds_write_b128 group (banks (a / 4) mod 32) whose items lie NC chunks apart then hit 8 distinct
+// 16-B slots when xm spreads them (xm from the lane's item index; 0 = plain order)
+template <typename T, int NC>
+__device__ __forceinline__ void nrm_st_chunks(T* p, const T* v, int xm) {
+  constexpr int VN = 16 / (int)sizeof(T);
+  T w[NC * VN];
+#pragma unroll
+  for (int i = 0; i < NC * VN; ++i) w[i] = v[i];
+  if (PCS_NRM_SWZ) {  // butterfly: w chunk k <- v chunk k ^ xm
+#pragma unroll
+    for (int b = 1; b < NC; b <<= 1) {
+      const bool sw = (xm & b) != 0;
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (!(j & b))
+#pragma unroll
+          for (int e = 0; e < VN; ++e) {
+            const T a = w[j * VN + e], c = w[(j | b) * VN + e];
+            w[j * VN + e] = sw ? c : a;
+            w[(j | b) * VN + e] = sw ? a : c;
+          }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    V16<T> c;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) c.v[e] = w[k * VN + e];
+    stv(p + VN * (PCS_NRM_SWZ ? (k ^ xm) : k), c);
+  }
+}
 template <typename T, int TX_, int RS_, int RB_, int PQ_>
 struct NrmG {
   static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
@@ -354,7 +390,11 @@ struct NrmG {
   // 2 (TX + PAD) +- PAD elements apart = an odd number of 16-B slots mod 256 B): every b128 lane group
   // then hits 16 distinct slots (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2,
   // profiles/r4_prof_c3f64_*).  A row never reaches the next one's first element.
-  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, WI = 4 * GI + PAD, TP = TX + PAD;
+  // fp32 with 8-output PH items: the 16 lanes of a group read every other 16-B slot of rows r and r + 1,
+  // so the staged rows take an odd slot pitch too (4 floats; 22.4 M bank-conflict cycles per 512^3
+  // launch without it, profiles/r4_prof_nrm32_pmc_summary.txt)
+  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, SPAD = sizeof(T) == 8 ? 2 : PQ == 2 ? 4 : 0;
+  static constexpr int WI = 4 * GI + SPAD, TP = TX + PAD;
   static __device__ __forceinline__ int rrow(int slot) { return slot * TP + ((slot >> 1) & 1) * PAD; }
   static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
   static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
@@ -549,7 +589,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       const int e = l * NT + tid, rr = e / GI, gg = e - rr * GI;
-      if (e < G::NIN) stq(stg + rr * WI + 4 * gg, q[l]);
+      // fp64: a group is 2 chunks, 8 lanes span 256 B: the second 4 lanes write their second chunk first
+      if (e < G::NIN) nrm_st_chunks<T, 4 / V16<T>::N>(stg + rr * WI + 4 * gg, q[l].v, (gg >> 2) & (4 / V16<T>::N - 1));
     }
   };
   auto issue = [&](const Cur& c, Q4<T>(&q)[NL]) {
@@ -604,12 +645,10 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       }
       int slot = sb + r;
       slot = slot >= RING ? slot - RING : slot;
-#pragma unroll
-      for (int p = 0; p < PQ; ++p) {
-        Q4<T> o;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) o.v[m] = acc[4 * p + m];
-        stq(ring + G::rrow(slot) + 4 * (g + p), o);
+      {  // NC chunks per item, items NC chunks apart: rotate by the item index's bits above 8 / NC lanes
+        constexpr int NC = 4 * PQ / V16<T>::N, LNC = NC >= 4 ? 2 : NC == 2 ? 1 : 0;
+        const int gi = e - r * GQ;
+        nrm_st_chunks<T, NC>(ring + G::rrow(slot) + 4 * g, acc, (gi >> (3 - LNC)) & (NC - 1));
       }
     }
     lds_barrier();
