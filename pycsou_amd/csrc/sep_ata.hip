@@ -344,8 +344,11 @@ static int ata_padb(int kb, int offb) {
 #ifndef PCS_NRM_PK  // fp32 PV taps as v_pk_fma_f32 on column pairs (tap broadcast); diagnostics
 #define PCS_NRM_PK 0
 #endif
-#ifndef PCS_NRM_SWZ  // lane-rotated 16-B chunk order of the LDS writes (below); diagnostics builds set 0
-#define PCS_NRM_SWZ 1
+// lane-rotated 16-B chunk order of the LDS writes (below): parity green, no measurable change (512^3 fp32
+// 0.463-0.478 against 0.454-0.487 ms, 1024^3 fp64 5.46-5.48 against 5.49, C4 631 it/s both ways,
+// profiles/r4_nrm_swz_ab.txt) -- off; diagnostics builds set 1
+#ifndef PCS_NRM_SWZ
+#define PCS_NRM_SWZ 0
 #endif
 
 // NC consecutive 16-B chunks v (chunk j at p + j 16 B) written in the lane's order k -> chunk k ^ xm: the 8
