@@ -153,7 +153,12 @@ constexpr int k3C0K = 15;
 #endif
 
 template <typename T, int FK, bool VEC>
-__global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
+// minimum resident workgroups per CU the register budget targets (non-fold kernels; diagnostics knob):
+// at 1 the fp64 kernel takes 157-169 VGPRs, 3 waves / SIMD = one 512-thread workgroup per CU
+#ifndef PCS_3D_MINB
+#define PCS_3D_MINB 1
+#endif
+__global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, FK == PCS_F_CONV0 ? 1 : PCS_3D_MINB) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
                                                  const T* __restrict__ z, T* __restrict__ zn,
                                                  const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk,
                                                  double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,

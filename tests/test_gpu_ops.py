@@ -508,11 +508,13 @@ def _c1_np(x, h, off, axis):
 
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 @pytest.mark.parametrize('ka,offa,kb,offb', [(15, 7, 15, 7), (15, 14, 15, 0), (6, 2, 9, 8), (3, 0, 5, 1), (1, 0, 2, 1)])
-@pytest.mark.parametrize('dims', [(4, 200, 264), (2, 1100, 128), (9, 17, 36), (3, 70, 4), (1, 5, 8), (12, 64, 256)])
+@pytest.mark.parametrize('dims', [(4, 200, 264), (2, 1100, 128), (9, 17, 36), (3, 70, 4), (1, 5, 8), (12, 64, 256),
+                                  (600, 64, 64), (40, 300, 260)])
 def test_conv2d_sep_ata_planes(A, dtype, ka, offa, kb, offb, dims):
     """pcs_conv2d_sep_ata_planes == C_a^T C_b^T C_b C_a per plane (four Convolve1D passes in
     NumPy, fp64): ragged strips and row segments, planes thinner than the 28-row vertical reach,
-    offsets that need the horizontal tap padding (kb=5, offb=1)."""
+    offsets that need the horizontal tap padding (kb=5, offb=1); more tasks than resident workgroups
+    (600 planes: one task per workgroup, later ones start as earlier ones finish)."""
     from pycsou_amd import _lib as L
     rng = np.random.default_rng(ka * 7 + kb + dims[2] + dims[1])
     xn = rng.standard_normal(dims)
