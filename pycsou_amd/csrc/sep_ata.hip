@@ -418,6 +418,9 @@ template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 1>; };
 #elif PCS_NRM_CFG == 2  // 256 threads, 8-output PH items
 template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
 template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
+#elif PCS_NRM_CFG == 5  // diagnostics: fp64 16-row steps, 128 threads (36 KB of LDS: 4 workgroups / CU)
+template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
+template <> struct NrmCfg<double> { using G = NrmG<double, 64, 16, 2, 2>; };
 #else  // diagnostics: 128 threads, RB 8 / 4 and 16 / 8-output PH items -- fewer LDS bytes per
        // output (38 against 77 B in fp32) but half the waves: 0.69 against 0.57 ms (512^3 fp32),
        // 9.4 against 7.8 ms (1024^3 fp64), profiles/r2_nrm_ablation.txt
