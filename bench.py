@@ -491,9 +491,10 @@ def leg_c3_f64(args, dtype, K, W, kind='forward'):
     """C3 at the reference's default precision, fp64 (x0 / z0 np.float, pycsou/opt/proxalgs.py:327,341;
     Gradient / Convolve2D dtype='float64', linop/diff.py:777, linop/conv.py:167): 4096^2, the same
     separable 15x15 blur.  fp64 takes the general-stencil engine's fp64 row march for every K kind:
-    N x = Conv^T Conv x by k_sep2d_nrm<double> into a buffer (2 words), then the march step
-    (k_pds2d_smarch<double>: reads x, N x, Conv^T y, z; writes x', z' -- 8 words).  Algorithmic bytes
-    of the iteration: 7 words x 8 B per pixel."""
+    grad F = N x - Conv^T y by k_sep2d_nrm<double> into a buffer (reads x, Conv^T y; writes grad F), then
+    the march step (k_pds2d_smarch<double>, GRADBUF: reads x, grad F, z; writes x', z' -- 7 words;
+    PCS_NX_SUB=0: N x alone, 2 words, and the subtraction in the step, 8 words).  Algorithmic bytes of
+    the iteration: 7 words x 8 B per pixel."""
     n = args.size
     dt = torch.float64
     t0 = time.perf_counter()
@@ -504,21 +505,26 @@ def leg_c3_f64(args, dtype, K, W, kind='forward'):
     N = n * n
     alg = 7 * N * 8
     km = r['kernels_ms']
+    sub = os.environ.get('PCS_NX_SUB', '1') != '0'
     res = {'workload': f'C3 TV-deconvolution {n}x{n} f64 (the reference default dtype), 15x15 Gaussian PSF (separable), '
-                       f'K = Gradient(kind={kind}), 0.05*L21Norm; grad F = N x - Conv^T y: N x by k_sep2d_nrm<double> '
-                       f'into a buffer + the fp64 general-stencil march step (k_pds2d_smarch<double>), back to back from C',
+                       f'K = Gradient(kind={kind}), 0.05*L21Norm; grad F = N x - Conv^T y: '
+                       + ('grad F by k_sep2d_nrm<double> (N x minus Conv^T y as it stores) into a buffer'
+                          if sub else 'N x by k_sep2d_nrm<double> into a buffer')
+                       + ' + the fp64 general-stencil march step (k_pds2d_smarch<double>), back to back from C',
            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
            'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'dtype': 'f64',
            'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
            'iteration_frac_of_hbm_peak': round(alg / (r['ms_per_step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if 'conv_nx' in km:
+        # the update's time = the iteration's minus N x timed alone (without the Conv^T y subtraction the
+        # in-iteration launch adds: the update is if anything under-credited)
         upd = km['step'] - km['conv_nx']
-        step_bytes = 8 * N * 8
-        res['roofline'] = {'bound': 'hbm', 'kernel': f'k_pds2d_smarch<double, {kind}, NB, L21> (update)',
+        step_bytes = (7 if sub else 8) * N * 8
+        res['roofline'] = {'bound': 'hbm', 'kernel': f'k_pds2d_smarch<double, {kind}, {"GRADBUF" if sub else "NB"}, L21> (update)',
                            'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
                            'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                            'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        res['nx_roofline'] = {'bound': 'hbm', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm<double>)',
+        res['nx_roofline'] = {'bound': 'hbm', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm<double>, timed alone)',
                               'kernel_ms': round(km['conv_nx'], 5), 'bytes_per_launch': 2 * N * 8,
                               'achieved': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9, 1),
                               'frac': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}

@@ -509,6 +509,9 @@ static bool sm_normal(const pcs_pds2d_args* a) {
 }
 
 static bool use_march(const pcs_pds2d_args* a);
+// sep_ata.hip: N x - sub by the two-pass normal-operator kernel (PCS_EUNSUPPORTED: taps / layout it does not take)
+int sep_normal_minus(int dt, const void* in, void* out, const void* sub, int64_t np, int64_t n1, int64_t n2,
+                     const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t st);
 
 // fp64 (the reference's default dtype): every K kind, the forward Gradient included, takes this march
 // (the forward-only fp32 kernels pds_pt.hpp / pds_nmarch.hpp have no fp64 form)
@@ -585,6 +588,21 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
     int64_t lo, hi;
     window_rows(a, a->halo_x, &lo, &hi);
     const int64_t off = (lo + a->halo_x) * a->n1;
+    // grad F = N x - Conv^T y formed by the normal-operator kernel itself (it reads Conv^T y as it stores): the
+    // step then reads one buffer (7 words instead of 8; the same subtraction, bit for bit).  PCS_NX_SUB=0
+    // (read once): N x alone and the subtraction in the step
+    static int nx_sub = -1;
+    if (nx_sub < 0) {
+      const char* e = getenv("PCS_NX_SUB");
+      nx_sub = e == nullptr || atoi(e) != 0;
+    }
+    if (nx_sub) {
+      const int rs = sep_normal_minus(a->dtype, (const T*)a->x + off, (T*)const_cast<void*>(a->gbuf) + off,
+                                      (const T*)a->cty + off, 1, hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half,
+                                      a->taps1, 2 * a->half + 1, a->half, st);
+      if (rs == PCS_OK) return launch_smarch<T, KK, PCS_F_GRADBUF>(a, rb, st);
+      if (rs != PCS_EUNSUPPORTED) return rs;
+    }
     const int rc = pcs_conv2d_sep_ata_planes(a->dtype, (const T*)a->x + off, (T*)const_cast<void*>(a->gbuf) + off, 1,
                                              hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half, a->taps1,
                                              2 * a->half + 1, a->half, st);

@@ -479,11 +479,27 @@ __device__ __forceinline__ double nrm_tap(const double* h, int k, int off, int d
   return (t >= 0 && t < k) ? h[t] : 0.0;
 }
 
+// 4 elements through a descriptor (16-B loads; an offset carrying kOOB reads 0)
 template <typename T>
+__device__ __forceinline__ Q4<T> nrm_bload(Rsrc r, uint32_t off) {
+  constexpr int VN = V16<T>::N;
+  Q4<T> a;
+#pragma unroll
+  for (int h = 0; h < 4 / VN; ++h) {
+    const auto d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off + 16 * h), 0, 0);
+    __builtin_memcpy(a.v + h * VN, &d, 16);
+  }
+  return a;
+}
+
+// SUB: out = C^T C in - sub (sub laid out as in / out; the fp64 2-D step's grad F = N x - Conv^T y formed
+// here, so the step reads one buffer instead of two -- the same subtraction, bit for bit)
+template <typename T, bool SUB>
 __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
                                                                  int n2, int nstrips, int nseg, int seg_len,
                                                                  int64_t ntasks, const T* __restrict__ ha_, int ka,
-                                                                 int offa, const T* __restrict__ hb_, int kb, int offb) {
+                                                                 int offa, const T* __restrict__ hb_, int kb, int offb,
+                                                                 const T* __restrict__ sub) {
   using G = typename NrmCfg<T>::G;
   constexpr int TX = G::TX, RS = G::RS, RB = G::RB, RING = G::RING, GX = G::GX, GI = G::GI, WI = G::WI, NT = G::NT,
                 NL = G::NL;
@@ -575,18 +591,6 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
     }
   };
-  // the step after c (more = false: none; c itself is returned)
-  auto advance = [&](const Cur& c, bool& more) {
-    Cur n = c;
-    more = true;
-    if (c.s + 1 < c.ns) {
-      n.s = c.s + 1;
-    } else {
-      more = c.t + t_stride < t_end;
-      if (more) n = task_at(c.t + t_stride);
-    }
-    return n;
-  };
   // the staged rows have landed (WAITN: the memory ops issued after them that may stay in flight --
   // vector memory ops retire in order); rows -> LDS
   auto stage = [&](const Q4<T>(&q)[NL], auto waitn) {
@@ -612,6 +616,17 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
   auto body = [&](const Cur cur) {
     const int vi = tid / GX, vg = tid - vi * GX;  // PV item: rows RB vi .. + RB - 1 of the step, group vg
     const int c0 = cur.strip * TX;
+    Q4<T> bsub[SUB ? RB : 1];  // SUB: the PV outputs' sub values, loaded before PH (a phase to land)
+    if constexpr (SUB) {
+      const Rsrc rs = rsrc_of(sub + cur.plane * (int64_t)n1 * n2, (uint32_t)((int64_t)n1 * n2 * sizeof(T)));
+      const int gc = c0 + 4 * vg;
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr) {
+        const int i = cur.a - 28 + cur.s * RS + RB * vi + rr;
+        const bool live = i >= cur.a && i < cur.b && gc < n2;
+        bsub[rr] = nrm_bload<T>(rs, live ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB);
+      }
+    }
     const int sb = (cur.s * RS) % RING;  // ring slot of the step's first staged row
     lds_barrier();
     // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q);
@@ -725,11 +740,27 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
             }
           }
         }
+        if constexpr (SUB) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[rr].v[m] = acc[rr].v[m] - bsub[rr].v[m];
+        }
         nrm_bstore(dst, live && !(PCS_NRM_ABL & 1) ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB, acc[rr]);
       }
     }
   };
 #if PCS_NRM_PF2
+  // the step after c (more = false: none; c itself is returned)
+  auto advance = [&](const Cur& c, bool& more) {
+    Cur n = c;
+    more = true;
+    if (c.s + 1 < c.ns) {
+      n.s = c.s + 1;
+    } else {
+      more = c.t + t_stride < t_end;
+      if (more) n = task_at(c.t + t_stride);
+    }
+    return n;
+  };
   // two register sets, the rows of step k + 2 issued at step k's top: at a step's top its own loads,
   // the previous two steps' stores and the next step's loads are in flight
   Q4<T> qa[NL], qb[NL];
@@ -782,11 +813,11 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #endif
 }
 
-template <typename T>
+template <typename T, bool SUB = false>
 static void nrm_attr() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep2d_nrm<T>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep2d_nrm<T, SUB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)NrmCfg<T>::G::lds_bytes());
     (void)hipGetLastError();
     done = true;
@@ -803,7 +834,7 @@ static int nrm_slots() {
                                                 hipSuccess || cus < 1)
       cus = 256;
     nrm_attr<T>();
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_nrm<T>, G::NT, G::lds_bytes()) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_nrm<T, false>, G::NT, G::lds_bytes()) != hipSuccess ||
         nb < 1)
       nb = 1;
     (void)hipGetLastError();
@@ -824,7 +855,7 @@ static bool nrm_fits(int64_t n1, int64_t n2, int ka, int offa, int kb, int offb)
 
 template <typename T>
 static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
-                   const void* hb, int kb, int offb, hipStream_t st) {
+                   const void* hb, int kb, int offb, hipStream_t st, const void* sub = nullptr) {
   using G = typename NrmCfg<T>::G;
   if (np == 0) return PCS_OK;
   const int64_t nstrips = (n2 + G::TX - 1) / G::TX, pieces = np * nstrips;
@@ -849,10 +880,17 @@ static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2
   }
   const int64_t gslots = gridx > 0 ? slots * gridx : ntasks;
   const int64_t grid = ntasks < gslots ? ntasks : gslots;
-  nrm_attr<T>();
-  k_sep2d_nrm<T><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>((const T*)in, (T*)out, (int)n1, (int)n2,
-                                                                (int)nstrips, (int)nseg, (int)seg_len, ntasks,
-                                                                (const T*)ha, ka, offa, (const T*)hb, kb, offb);
+  if (sub != nullptr) {
+    nrm_attr<T, true>();
+    k_sep2d_nrm<T, true><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>(
+        (const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg, (int)seg_len, ntasks, (const T*)ha, ka, offa,
+        (const T*)hb, kb, offb, (const T*)sub);
+  } else {
+    nrm_attr<T>();
+    k_sep2d_nrm<T, false><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>(
+        (const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg, (int)seg_len, ntasks, (const T*)ha, ka, offa,
+        (const T*)hb, kb, offb, nullptr);
+  }
   return launch_status();
 }
 
@@ -904,6 +942,22 @@ static int sep_ata(const void* in, void* out, int64_t np, int64_t n1, int64_t n2
 }  // namespace pcs
 
 using namespace pcs;
+
+namespace pcs {
+// N x - sub by the two-pass kernel (the fp64 2-D march's gradient buffer, pds.hip); PCS_EUNSUPPORTED when
+// the two-pass kernel does not take the taps / layout (the caller then forms N x and subtracts in the step)
+int sep_normal_minus(int dt, const void* in, void* out, const void* sub, int64_t np, int64_t n1, int64_t n2,
+                     const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t st) {
+  if (!in || !out || !sub || !ha || !hb || np < 0 || n1 < 1 || n2 < 1 || in == out || sub == out) return PCS_EINVAL;
+  if ((uintptr_t)in % 16 || (uintptr_t)out % 16 || (uintptr_t)sub % 16) return PCS_EINVAL;
+  const int64_t esz = dt == PCS_F64 ? 8 : 4;
+  if (!nrm_fits(n1, n2, ka, offa, kb, offb) || n1 * n2 * esz >= (1LL << 30)) return PCS_EUNSUPPORTED;
+  if (np == 0) return PCS_OK;
+  if (dt == PCS_F32) return sep_nrm<float>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st, sub);
+  if (dt == PCS_F64) return sep_nrm<double>(in, out, np, n1, n2, ha, ka, offa, hb, kb, offb, st, sub);
+  return PCS_EINVAL;
+}
+}  // namespace pcs
 
 extern "C" {
 
