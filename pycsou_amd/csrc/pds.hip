@@ -462,6 +462,10 @@ static int sm_slots() {
       nb = sizeof(T) == 4 ? 3 : 2;
     (void)hipGetLastError();
     slots = cus * (nb < 3 ? nb : 3);
+    // fp64: three rounds of the resident workgroups (later ones start as earlier ones finish), with
+    // segments of >= 8 steps (sm_plan).  fp64 C3 4096^2: 3326-3379 it/s against 3194-3219 at one round,
+    // 3139-3226 at four or six (profiles/r4_f64_step_slots.txt)
+    if (sizeof(T) == 8) slots *= 3;
     const char* e = getenv("PCS_SM_SLOTS");  // diagnostics: grid-size sweep
     if (e && atoi(e) > 0) slots = atoi(e);
   }
@@ -483,8 +487,8 @@ static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tiles_x = (int)((a->n1 + 63) / 64);
   if (tiles_x < 2) return false;
   const int rs = sm_rs(a);
-  // at least 4 16-row halves per segment (2 steps of 32 rows)
-  plan_bands(rb, 16 * rs, tiles_x, sm_slots_for(a, rs), 4 / rs, p);
+  // at least 4 16-row halves per segment (2 steps of 32 rows); fp64 at least 8 steps
+  plan_bands(rb, 16 * rs, tiles_x, sm_slots_for(a, rs), a->dtype == PCS_F64 ? 8 : 4 / rs, p);
   return true;
 }
 
