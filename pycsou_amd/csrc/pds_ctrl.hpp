@@ -77,6 +77,17 @@ struct RedOut {
 // run while the side stream's loop control writes the flag, so thread 0's reading is broadcast
 // and every workgroup still arrives at the reduction counters (with zero partials), which
 // then stay consistent for the next run of the plan.
+// Single-GPU launches (no sums output) read the stop flag at entry but consume it inside the task, after
+// the task's first loads have issued (PCS_DEFER_STOP): the flag's latency overlaps theirs instead of
+// preceding them.  The task returns before its first store when the flag is set.
+#ifndef PCS_DEFER_STOP
+#define PCS_DEFER_STOP 1
+#endif
+__device__ __forceinline__ bool stop_deferred(const RedOut& ro) { return PCS_DEFER_STOP && ro.sums == nullptr; }
+__device__ __forceinline__ int stop_flag_early(const Ctrl* ctrl, const RedOut& ro) {
+  return stop_deferred(ro) && ctrl != nullptr ? ctrl->stopped : 0;
+}
+
 __device__ __forceinline__ bool stop_requested(const Ctrl* ctrl, const RedOut& ro, int* flag) {
   if (ctrl == nullptr) return false;
   if (ro.sums == nullptr) return ctrl->stopped != 0;

@@ -204,7 +204,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
                                             T* __restrict__ zn, const T* __restrict__ b,
                                             const T* __restrict__ tq, const Slab32& s, const Params<T>& P, int gk,
                                             int edge, int s0, int s1, int c0, T* sm, T* Z0, T* Z1,
-                                            double (&part)[4]) {
+                                            double (&part)[4], int stop_raw) {
   static_assert(sizeof(T) == 4 && NT == 256, "fp32, 256 threads (4 rows x 16 column groups per wave)");
   constexpr bool GEN = KK != PCS_FORWARD;
   using M = NMarch<H, GEN>;
@@ -950,6 +950,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #endif
     vm_wait<0>();
   }
+  if (stop_raw) return;  // loop already stopped (solver.py:65-66): loads landed, nothing stored
   lds_barrier();
   ph(s0 - 2 * H - PR + ui);  // t rows [s0 - 2H - PR, s0 - 2H - PR + 16)
   if (ui + TS < 4 * H + 1 + PR) ph(s0 - 2 * H - PR + TS + ui);  // t rows [.. + 16, s0 + 2H]
@@ -1042,7 +1043,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];  // into them never aliases a ring read
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
-  const bool stopped = stop_requested(ctrl, ro, flag);
+  const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
+  const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
@@ -1056,7 +1058,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  if (!stopped) nmarch_task<T, H, HK, NT, PCS_FORWARD>(x, xn, z, zn, b, tq, s, P, gk, 0, s0, s1, c0, sm, zs0, zs1, part);
+  if (!stopped)
+    nmarch_task<T, H, HK, NT, PCS_FORWARD>(x, xn, z, zn, b, tq, s, P, gk, 0, s0, s1, c0, sm, zs0, zs1, part, stop_raw);
+  if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
@@ -1080,7 +1084,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
-  const bool stopped = stop_requested(ctrl, ro, flag);
+  const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
+  const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
@@ -1094,7 +1099,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   const int c0 = strip * M::TW;
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
-  if (!stopped) nmarch_task<T, H, HK, NT, KK>(x, xn, z, zn, b, tq, s, P, gk, edge, s0, s1, c0, sm, zs0, zs1, part);
+  if (!stopped) nmarch_task<T, H, HK, NT, KK>(x, xn, z, zn, b, tq, s, P, gk, edge, s0, s1, c0, sm, zs0, zs1, part, stop_raw);
+  if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);

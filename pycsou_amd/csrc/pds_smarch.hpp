@@ -130,7 +130,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
                                             const T* __restrict__ msrc, T* __restrict__ mdst,
                                             const Slab32& s, const Params<T>& P,
                                             const SParamsT<T>& Q, int gk, int s0, int s1, int c0, T* sm,
-                                            double (&part)[4]) {
+                                            double (&part)[4], int stop_raw) {
   constexpr uint32_t ES = sizeof(T);
   constexpr int SAUX = sizeof(T) == 4 ? PCS_SM_SAUX : PCS_SM_SAUX64;
   using M = SMarch<KK, RS>;
@@ -444,6 +444,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
     loads_x(P1{}, s0, -(1 << 30));
   }
 #endif
+  if (stop_raw) return;  // loop already stopped (solver.py:65-66): loads issued, nothing stored
   lds_barrier();
   uphase(std::false_type{}, P0{}, s0 - TS);
   // step k reads register set PB = (k + 1) & 1 and loads the other one for step k + 1
@@ -502,7 +503,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   __shared__ __attribute__((aligned(16))) T sm[SMarch<KK, RS>::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
-  const bool stopped = stop_requested(ctrl, ro, flag);
+  const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
+  const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
   int task;
   {  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
@@ -516,10 +518,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
     if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
-      smarch_task<T, KK, FK, HK, true, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, true, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
+                                           stop_raw);
     else
-      smarch_task<T, KK, FK, HK, false, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part);
+      smarch_task<T, KK, FK, HK, false, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
+                                            stop_raw);
   }
+  if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
   if (hist != nullptr || ro.sums != nullptr) {
     reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
