@@ -129,7 +129,18 @@ __device__ __forceinline__ void gstore(T* p, const G4<T>& g, int c, int n2) {
 #endif
 // 8 x 128 tiles: a 64-column tile's one-group right halo costs a third 128-B line per row
 // (PMC: 1.53x the algorithmic reads); at 128 columns it is one line in five
-constexpr int k3T1 = 8, k3TW = PCS_K3TW, k3NT = PCS_K3TW == 64 ? 256 : PCS_K3TW == 128 ? 512 : 1024;
+constexpr int k3T1 = 8, k3TW = PCS_K3TW;
+// fp64 forward-K tile width (diagnostics builds override): 64 columns = 256-thread workgroups, three of
+// them per CU at the fp64 kernel's 157-169 VGPRs instead of one 512-thread one -- measured slower (C5
+// update 17.0 against 14.9 ms, profiles/r4_c5_tile64_ab.txt): 128 stays
+#ifndef PCS_K3TW64
+#define PCS_K3TW64 PCS_K3TW
+#endif
+template <typename T>
+struct K3 {
+  static constexpr int TW = sizeof(T) == 8 ? PCS_K3TW64 : PCS_K3TW;
+  static constexpr int NT = TW == 64 ? 256 : TW == 128 ? 512 : 1024;
+};
 
 // fkind PCS_F_CONV0: grad F = C0^T (C0 t - w) along axis 0 inside the update, t (the `g` array) the
 // in-plane normal operator C12^T C12 x and w = C12^T y: per U item two 15-plane register rings
@@ -158,7 +169,7 @@ template <typename T, int FK, bool VEC>
 #ifndef PCS_3D_MINB
 #define PCS_3D_MINB 1
 #endif
-__global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, FK == PCS_F_CONV0 ? 1 : PCS_3D_MINB) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
+__global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK == PCS_F_CONV0 ? 1 : PCS_3D_MINB) void k_pds3d(const T* __restrict__ x, T* __restrict__ xn,
                                                  const T* __restrict__ z, T* __restrict__ zn,
                                                  const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk,
                                                  double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, FK == PCS_F_CO
                                                  int off0) {
   // PCS_F_CONV0: a second set of k3NT threads (waves 8-15) runs the axis-0 rings beside the update
   constexpr bool FOLD = FK == PCS_F_CONV0;
-  constexpr int T1 = k3T1, TW = k3TW, NT = FOLD ? 2 * k3NT : k3NT;
+  constexpr int T1 = k3T1, TW = K3<T>::TW, NT = FOLD ? 2 * K3<T>::NT : K3<T>::NT;
   constexpr int UR = T1 + 1, WG = TW + 4, GG = WG / 4;
   constexpr int NU = UR * GG;                 // U items (x_t / u), 153
   constexpr int NZ = T1 * (TW / 4);           // z' items, 128
@@ -224,8 +235,8 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, FK == PCS_F_CO
   constexpr int UWAVES = (NU + 63) / 64, NRI = UR * WG / RV;
   // first ring thread: the update loop's item-free waves join the ring waves when RV = 2
   constexpr int IWAVES = (cmax(cmax(NU, NZ), cmax(NZ1, NZ2)) + 63) / 64;  // waves holding update items
-  constexpr int RBASE = RV == 2 ? 64 * IWAVES : k3NT;
-  static_assert(!FOLD || (WG % RV == 0 && NRI <= NT - RBASE && RBASE <= k3NT && 64 * IWAVES <= RBASE),
+  constexpr int RBASE = RV == 2 ? 64 * IWAVES : K3<T>::NT;
+  static_assert(!FOLD || (WG % RV == 0 && NRI <= NT - RBASE && RBASE <= K3<T>::NT && 64 * IWAVES <= RBASE),
                 "ring items: whole rows, one per ring thread, none on a wave with update items");
   __shared__ __attribute__((aligned(16))) T GS[2][FOLD ? SZU : 4];
   const bool ring_wave = FOLD && tid >= RBASE;  // wave-uniform
@@ -847,7 +858,10 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   if (pb.b0 == pb.a0) pb = PlaneBands{pb.a1, pb.b1, pb.b1, pb.b1};
   const int t1 = tile_rows3(a);
   p.tiles1 = (int)((a->n1 + t1 - 1) / t1);
-  p.tiles2 = (int)((a->n2 + k3TW - 1) / k3TW);
+  const int tw = (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) ? k3gTW
+                 : a->dtype == PCS_F32                                  ? K3<float>::TW
+                                                                        : K3<double>::TW;
+  p.tiles2 = (int)((a->n2 + tw - 1) / tw);
   const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
   const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
   const int64_t bands = (L0 > 0) + (L1 > 0);
@@ -910,7 +924,7 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   }
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
-  static_assert(k3gTW == k3TW, "the general-K kernel shares the forward kernel's column tiles");
+  static_assert(k3gTW == k3TW, "the general-K kernel keeps the fp32 forward kernel's column tiles");
   if constexpr (FK != PCS_F_CONV0) {
     if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
       auto kern =
@@ -921,7 +935,7 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
       return launch_status();
     }
   }
-  k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, FK == PCS_F_CONV0 ? 2 * k3NT : k3NT, 0, st>>>(
+  k_pds3d<T, FK, VEC><<<(unsigned)p.ntasks, FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, 0, st>>>(
       (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g, v, P, a->hkind, a->gkind, a->partials,
       (Ctrl*)a->ctrl, a->hist, a->ws, p.tiles1, p.tiles2, p.bd, p.ntasks, (const T*)a->conv0_w,
       (const T*)a->conv0_taps, a->conv0_k, a->conv0_off);
