@@ -393,10 +393,10 @@ struct NrmG {
   // 2 (TX + PAD) +- PAD elements apart = an odd number of 16-B slots mod 256 B): every b128 lane group
   // then hits 16 distinct slots (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2,
   // profiles/r4_prof_c3f64_*).  A row never reaches the next one's first element.
-  // fp32 with 8-output PH items: the 16 lanes of a group read every other 16-B slot of rows r and r + 1,
-  // so the staged rows take an odd slot pitch too (4 floats; 22.4 M bank-conflict cycles per 512^3
-  // launch without it, profiles/r4_prof_nrm32_pmc_summary.txt)
-  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, SPAD = sizeof(T) == 8 ? 2 : PQ == 2 ? 4 : 0;
+  // fp32 with 8- / 16-output PH items: the lanes of a group read every other (every fourth) 16-B slot of
+  // rows r, r + 1 (.. r + 3), so the staged rows take an odd slot pitch too (4 floats; 22.4 M bank-conflict
+  // cycles per 512^3 launch without it at 8 outputs, profiles/r4_prof_nrm32_pmc_summary.txt)
+  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, SPAD = sizeof(T) == 8 ? 2 : PQ >= 2 ? 4 : 0;
   static constexpr int WI = 4 * GI + SPAD, TP = TX + PAD;
   static __device__ __forceinline__ int rrow(int slot) { return slot * TP + ((slot >> 1) & 1) * PAD; }
   static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
@@ -406,16 +406,20 @@ struct NrmG {
   static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TP + NTAB); }
 };
 template <typename T> struct NrmCfg;
-// 8-output PH items (PQ 2) since round 4: 512^3 fp32 0.483 against 0.495-0.500 ms, 1024^3 fp64 5.32-5.34
-// against 5.52-5.57 ms, 4096^2 fp64 0.105-0.107 against 0.108-0.109 ms (profiles/r4_nrm_var_ab.txt);
-// PCS_NRM_CFG=0 (diagnostics) the 4-output items
+// wider PH items since round 4 -- 8 outputs (PQ 2): 512^3 fp32 0.483 against 0.495-0.500 ms, 1024^3 fp64
+// 5.32-5.34 against 5.52-5.57 ms, 4096^2 fp64 0.105-0.107 against 0.108-0.109 ms (profiles/r4_nrm_var_ab.txt);
+// fp32 16 outputs (PQ 4): 0.433-0.449 against 0.469 ms, C4 642-645 against 633-635 it/s
+// (profiles/r4_nrm_cfg6_ab.txt).  PCS_NRM_CFG=0 (diagnostics): the 4-output items
 #ifndef PCS_NRM_CFG
 #define PCS_NRM_CFG 2
 #endif
 #if PCS_NRM_CFG == 0
 template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 1>; };
 template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 1>; };
-#elif PCS_NRM_CFG == 2  // 256 threads, 8-output PH items
+#elif PCS_NRM_CFG == 2  // 256 threads, 16-output (fp32) / 8-output (fp64) PH items
+template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 4>; };
+template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
+#elif PCS_NRM_CFG == 6  // diagnostics: fp32 8-output PH items
 template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
 template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
 #elif PCS_NRM_CFG == 5  // diagnostics: fp64 16-row steps, 128 threads (36 KB of LDS: 4 workgroups / CU)
