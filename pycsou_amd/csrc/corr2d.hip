@@ -564,7 +564,9 @@ static int slots_for() {
                                                      Cfg<T, K>::LDS_BYTES) != hipSuccess ||
         nb < 1)
       nb = 1;
-    return cus * nb;
+    const char* e = getenv("PCS_CORR_ROUNDS");  // diagnostics: rounds of the resident workgroups
+    const int rounds = e && atoi(e) > 0 ? atoi(e) : 1;
+    return cus * nb * rounds;
   }();
   return slots;
 }
