@@ -236,6 +236,7 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
     (barrier + synchronize on both sides, max over ranks)."""
     from pycsou_amd.opt.engine3d import PDS3DEngine
     from pycsou_amd.parallel import DistComm
+    from pycsou_amd.parallel.slab import comm_probe
     t0 = time.perf_counter()
     pds = build_volume(n, dtype, kind=kind)
     spec = pds._fused_spec()
@@ -267,6 +268,9 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
         t = torch.tensor([dt], dtype=torch.float64, device='cuda' if dist.get_backend() == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # after the timed region: the compute, the sums all-gather and the halo exchange timed apart
+    # (idempotent re-runs on the final iterate, max over ranks), so a scaling run explains itself
+    probe = comm_probe(eng) if world > 1 else None
     ms = dt * 1e3 / K
     elem = torch.empty(0, dtype=dtype).element_size()
     alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
@@ -284,6 +288,7 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
            'banded_order': ((eng.order if eng.overlap else 'serial') if getattr(eng, 'banded', False) else None)
                            if world > 1 else None,
            'order_trial_ms': getattr(eng, 'tune_ms', None),
+           'comm': probe,
            'setup_s': round(t1 - t0, 1)}
     del eng
     if comm is not None:
@@ -625,6 +630,7 @@ def slab_bench(n, dtype, K, W, world):
     """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
     (barrier + synchronize on both sides; the caller takes the max over ranks)."""
     from pycsou_amd.parallel import DistComm, SlabPDS2D
+    from pycsou_amd.parallel.slab import comm_probe
     pds = build_problem(n * world, n, dtype, lipschitz='analytic')
     comm = DistComm() if world > 1 else None
     kw = dict(rank=0 if comm is None else None, world=1 if comm is None else None)
@@ -671,11 +677,13 @@ def slab_bench(n, dtype, K, W, world):
         t = torch.tensor([dt], dtype=torch.float64, device='cuda' if dist.get_backend() == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    probe = comm_probe(eng) if world > 1 else None  # compute / all-gather / exchange timed apart
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
     loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else (
         'python (gloo rehearsal)' if world > 1 and dist.get_backend() != 'nccl' else 'python')
     return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks,
-            'loop': loop, 'loop_fallback': fallback, 'schedule_trial_ms': getattr(eng, 'tune_ms', None)}
+            'loop': loop, 'loop_fallback': fallback, 'schedule_trial_ms': getattr(eng, 'tune_ms', None),
+            'comm': probe}
 
 
 def _free_port():
@@ -773,7 +781,7 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:10,c4_cen:512:f32:20:centered',
+    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:20,c4_cen:512:f32:20:centered',
                     help='volume legs name:edge:dtype:steps[:kind], comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
     ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,c3_f64,c3_cen_f64,conv63,cps_inpaint',
@@ -895,6 +903,7 @@ def main():
         if 'loop' in res:  # multi-GPU: which slab loop ran (native RCCL loop, or the torch.distributed fallback)
             out['loop'] = res['loop']
             out['loop_fallback'] = res['loop_fallback']
+            out['comm'] = res.get('comm')  # compute / all-gather / exchange ms, halo GB/s per side
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(n, args.cpu_iters)
         else:
@@ -923,19 +932,22 @@ def main():
 
 def volume_leg(args, out, key, edge, dtype_v, steps, world, rank, kind='forward'):
     """Run volume_bench under a watchdog; `out` (rank 0) gains `key`.  A failure leaves the C3
-    line as it was; a stall past --volume-timeout prints it and ends the process."""
+    line as it was; a stall past --volume-timeout prints it (with the leg's `error`) and ends the
+    process with status 1, so a hung leg is never mistaken for a clean run."""
     def fire():
         if out is not None:
             out[key] = {'error': f'no result within {args.volume_timeout:.0f} s'}
             print(json.dumps(out), flush=True)
         sys.stderr.write('bench: volume leg timed out\n')
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(1)
     timer = threading.Timer(args.volume_timeout, fire)
     timer.daemon = True
     timer.start()
     try:
         K = max(2, steps + steps % 2)
+        if os.environ.get('PCS_BENCH_TEST_STALL') == key:  # tests only: a leg that never returns
+            time.sleep(1e6)
         vres = volume_bench(edge, dtype_v, K, 8, world, rank, kind)  # warmup also picks the schedule
     except Exception as e:  # noqa: BLE001 -- the C3 line stands on its own
         vres = {'error': f'{type(e).__name__}: {e}'[:300]}

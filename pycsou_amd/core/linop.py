@@ -32,11 +32,11 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     The run stops when r <= tol |theta|, when theta moved by at most ``tol`` (relative) since
     the previous check, or on an invariant subspace (beta ~ 0).
 
-    Returns theta + r when the residual test stopped the run (r <= tol |theta|: some eigenvalue lies
-    within r of the Ritz value, so the value errs by at most tol on the high side -- no guaranteed
-    upper bound on the extreme eigenvalue, since that eigenvalue need not be the one near theta),
-    and theta itself when it stopped on stagnation or an invariant subspace (a Ritz value never
-    exceeds the extreme eigenvalue; stagnation to tol means it is within about tol of it).  The
+    Returns theta + r when the residual test or stagnation stopped the run (some eigenvalue lies
+    within r of the Ritz value; a Ritz value never exceeds the extreme eigenvalue, so the value
+    stays on the high side of theta, which keeps tau sigma ||K||^2 <= 1 on the safe side even
+    without re-orthogonalisation), and theta itself on an invariant subspace (r = 0: theta is an
+    eigenvalue of A).  The
     structured operators of the path (Gradient, derivatives, separable / 1-D convolutions) do not
     come here: their norms are exact (linop/_spectral.py).
     """
@@ -85,7 +85,7 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
         if resid <= tol * abs(theta):
             return theta + resid
         if prev is not None and abs(theta - prev) <= tol * abs(theta):
-            return theta
+            return theta + resid
         prev = theta
     return theta + resid
 

@@ -953,7 +953,9 @@ namespace pcs {
 int sep_normal_minus(int dt, const void* in, void* out, const void* sub, int64_t np, int64_t n1, int64_t n2,
                      const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t st) {
   if (!in || !out || !sub || !ha || !hb || np < 0 || n1 < 1 || n2 < 1 || in == out || sub == out) return PCS_EINVAL;
-  if ((uintptr_t)in % 16 || (uintptr_t)out % 16 || (uintptr_t)sub % 16) return PCS_EINVAL;
+  // a buffer off the 16-B grid is a layout this kernel does not take: the caller's fallback (N x, then the
+  // subtraction inside the step) runs it
+  if ((uintptr_t)in % 16 || (uintptr_t)out % 16 || (uintptr_t)sub % 16) return PCS_EUNSUPPORTED;
   const int64_t esz = dt == PCS_F64 ? 8 : 4;
   if (!nrm_fits(n1, n2, ka, offa, kb, offb) || n1 * n2 * esz >= (1LL << 30)) return PCS_EUNSUPPORTED;
   if (np == 0) return PCS_OK;

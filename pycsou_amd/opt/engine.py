@@ -697,6 +697,13 @@ def match_masked_stencil2d(F, G, H, K, has_H):
     n0, n1 = spec['shape']
     if M.shape[1] != n0 * n1 or n1 % 4 or n1 <= 64:
         return None
+    # the fused block marks unsampled pixels by a NaN in the expanded data: data that is not finite
+    # itself would be read as unsampled there, so it takes the generic path (which propagates it, as
+    # the reference's L1Loss prox does)
+    sh = h_loss.shift
+    finite = bool(torch.isfinite(sh).all().item()) if isinstance(sh, torch.Tensor) else bool(np.isfinite(sh).all())
+    if not finite:
+        return None
     spec['mask'] = M.sampling_bool
     spec['mask_shift'] = h_loss.shift  # = -y
     spec['m'] = m

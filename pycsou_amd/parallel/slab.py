@@ -711,6 +711,53 @@ class SlabPDS2D:
         return float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
 
+def comm_probe(eng, reps=5):
+    """Where one rank's multi-GPU iteration spends its time: the compute alone (the step +
+    the partial-sum reduction on the whole slab), the sums all-gather alone and the halo
+    exchange alone, each re-run `reps` times on the current iterate and timed by HIP events
+    on the current stream (max over ranks).  Every phase is idempotent there: compute(p)
+    rewrites the parity-(1 - p) buffers from the parity-p ones, the all-gather and the
+    exchange re-send values already in place -- the iterate and the loop control are left as
+    they were.  `eng`: a SlabPDS2D or a multi-rank PDS3DEngine (the loop being
+    sharded is pycsou/core/solver.py:55-76).  Returns a dict of ms per phase, the halo bytes one
+    side sends per iteration and the exchange's achieved GB/s per side."""
+    if eng.world == 1 or eng.comm is None:
+        return None
+    comm = eng.comm
+    if isinstance(comm, DistComm) and getattr(eng, 'native', False):
+        comm = comm.rccl() or comm  # the 2-D native loop moves its halos through the library's RCCL binding
+    p = eng._p
+    pairs = eng.halos[p]
+    side = next(iter(pairs.values()), [])
+    halo = int(sum(s.numel() * s.element_size() for s, _ in side))
+    phases = {
+        'compute_ms': lambda: eng._compute(p),
+        'allgather_ms': lambda: comm.allgather(eng.sums, eng.gathered),
+        'exchange_ms': lambda: comm.exchange(pairs),
+    }
+    out = []
+    for name, fn in phases.items():
+        fn()  # untimed once
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) / reps)
+    dev = eng.sums.device
+    mine = torch.tensor(out + [0.0], dtype=torch.float64, device=dev)
+    allt = torch.zeros(4 * eng.world, dtype=torch.float64, device=dev)
+    comm.allgather(mine, allt)
+    worst = allt.view(eng.world, 4).max(dim=0).values[:3].tolist()
+    res = {k: round(v, 4) for k, v in zip(phases, worst)}
+    res['halo_bytes_per_side'] = halo
+    res['exchange_GBps_per_side'] = round(halo / (res['exchange_ms'] * 1e-3) / 1e9, 2) if res['exchange_ms'] > 0 else None
+    res['reps'] = reps
+    return res
+
+
 def run_local(slabs, max_iter, min_iter, accuracy_threshold, split=False):
     """Drive all slabs of one image inside one process (device-to-device halo copies);
     the per-iteration phase order is the distributed one.  ``split``: each slab's step runs

@@ -60,9 +60,28 @@ def test_world_size_mismatch_fails():
 def test_self_launch_slab_headline_gloo_one_gpu():
     """The real N = 2 slab headline on one GPU (two gloo ranks): n_gpus 2, slab2, the designed
     torch.distributed loop (no fallback)."""
-    p = _run(['--gpus', '2', '--steps', '6', '--warmup', '2', '--size', '512', '--volumes', '', '--legs', '',
+    p = _run(['--gpus', '2', '--steps', '6', '--warmup', '2', '--size', '512', '--volumes', 'c4:128:f32:20', '--legs', '',
               '--no-cpu-baseline', '--headline-timeout', '100'], {'PCS_BENCH_BACKEND': 'gloo'}, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json_line(p.stdout)
     assert d['n_gpus'] == 2 and d['config']['parallelism'] == 'slab2'
     assert d['loop_fallback'] is False and d['value'] > 0
+    # the multi-GPU lines explain themselves: compute / all-gather / exchange timed apart
+    for probe in (d['comm'], d['volume_c4']['comm']):
+        for k in ('compute_ms', 'allgather_ms', 'exchange_ms'):
+            assert probe[k] > 0, probe
+        assert probe['halo_bytes_per_side'] > 0 and probe['exchange_GBps_per_side'] > 0, probe
+    v = d['volume_c4']
+    assert v['steps'] == 20 and v['it_per_s'] > 0, v
+    assert v['halo_bytes_per_side_per_iter'] == v['comm']['halo_bytes_per_side'], v
+
+
+@pytest.mark.gpu
+def test_volume_leg_stall_exits_nonzero():
+    """A volume leg that never returns: the watchdog prints the line with the leg's error and the
+    process exits 1 (a hung first RCCL run must not read as a clean one)."""
+    p = _run(['--steps', '4', '--warmup', '2', '--size', '256', '--volumes', 'c4:64:f32:2', '--legs', '',
+              '--no-cpu-baseline', '--volume-timeout', '5'], {'PCS_BENCH_TEST_STALL': 'volume_c4'}, timeout=110)
+    assert p.returncode == 1, (p.returncode, p.stderr[-2000:])
+    d = _json_line(p.stdout)
+    assert d['value'] > 0 and 'error' in d['volume_c4'], d
