@@ -324,14 +324,6 @@ int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int6
  * (even n leaves the iterate in x, z); requires hist/ctrl/ws (in-kernel loop control).  The
  * host-side form of GenericIterativeAlgorithm.iterate's loop (pycsou/core/solver.py:55-76). */
 int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t stream);
-/* The same n iterations in one persistent launch (fp32 pointwise-F family: NULL / DENOISE /
-   GRADBUF; whole image), one grid barrier per iteration instead of a kernel boundary.
-   `bar`: pcs_grid_bar_bytes() device bytes, reset on `stream` at the start of every call;
-   bar[64] (uint32) != 0 after the run = barrier timeout (grid not co-resident): the iterate
-   and the loop control are then invalid and the caller must discard them.  Replaces the same
-   loop as pcs_pds2d_run (pycsou/core/solver.py:55-76).  -3 when not applicable. */
-int pcs_pds2d_run_persistent(const pcs_pds2d_args* a, int64_t n, void* bar, hipStream_t stream);
-int64_t pcs_grid_bar_bytes(void);
 
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics (pycsou/opt/proxalgs.py:343-394)
  * for a 2-D image with a general finite-difference K (single GPU, whole image):

@@ -139,8 +139,6 @@ _SIGS = {
     'pcs_pds2d_stencil_ws_bytes': (_c_i64, [ctypes.POINTER(StencilArgs)]),
     'pcs_pds2d_stencil_step': (_c_int, [ctypes.POINTER(StencilArgs), _vp]),
     'pcs_pds2d_stencil_run': (_c_int, [ctypes.POINTER(StencilArgs), _c_i64, _vp]),
-    'pcs_pds2d_run_persistent': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp, _vp]),
-    'pcs_grid_bar_bytes': (_c_i64, []),
     'pcs_pds2d_nblocks_bands': (_c_i64, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64]),
     'pcs_pds2d_step_bands': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _c_i64, _c_i64, _c_i64, _vp]),
     'pcs_comm_available': (_c_int, []),
@@ -177,7 +175,7 @@ class HipError(ValueError):
 
 
 # the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def load():

@@ -325,223 +325,6 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
   }
 }
 
-// ---------------------------------------------------------------- fp32 packed form
-// Two output rows per thread, v_pk_fma_f32: an input row q of the window feeds output row r with tap
-// row q and output row r + 1 with tap row q - 1, so one packed FMA updates (out[r][c], out[r+1][c])
-// with the tap pair (w[q][j], w[q-1][j]) (zero past either end) and the input x[r+q][c+j] broadcast
-// to both lanes (op_sel: any register, no pair moves).  Each lane's sequence of fmaf is the scalar
-// kernel's, in the same order (plus one fma with a zero tap at either end), so the sums match it.
-// The idea: a wave64 v_fma_f32 issues every 2 cycles only with two waves alternating on the SIMD
-// (4 alone), and the scalar kernel sits at 2 waves / SIMD (VALU ~53 % busy, PMC r3_prof_corr); one
-// v_pk_fma_f32 does two lanes' worth in the 4 cycles, so one wave would keep the SIMD's FP32 rate.
-// Measured slower (use_pk below): opt-in diagnostics only.
-// Geometry: 256 threads = 32 row pairs x 8 chunks of 8 columns (a 64-column strip, 64-row blocks);
-// a b128 lane group (16 lanes) reads 2 row pairs x 8 chunks: rows 2 apart, so the ring stores row
-// slot s at s * PB + (s >> 1) * 16 -- the second row of the group then sits an odd number of 16-B
-// bank slots away from the first and the 16 lanes hit 16 distinct slots (the chunks are 32 B apart).
-namespace corr2d {
-template <int K>
-struct PkCfg {
-  static constexpr int V = 4, CW = 8, TW = 64, TH = 64, Kc = K / 2;
-  static constexpr int LEFT = (Kc + V - 1) / V * V;            // LDS col 0 = strip col 0 - LEFT
-  static constexpr int NB = (LEFT + CW + Kc + V - 1) / V;       // b128 reads per thread per input row
-  static constexpr int WIN = NB * V;
-  static constexpr int PL = (TW - CW) + WIN;                    // logical row width
-  static constexpr int PV = PL / V;
-  static constexpr int PB = (PL * 4 + 15) / 16 * 16;            // row pitch (bytes)
-  static constexpr int RS = (TH + K - 1 + 15) / 16 * 16;        // ring rows (even)
-  static constexpr int KP2 = (K + 1) / 2 * 2;                   // tap pairs per input row (b128 = 2 pairs)
-  static constexpr int RING_BYTES = RS * PB + (RS / 2) * 16;
-  static constexpr int LDS_BYTES = RING_BYTES + (K + 2) * KP2 * 8;  // tap rows 0..K + a spare (zero) row
-  static constexpr int NPRE = (TH * PV + 255) / 256;
-};
-__device__ __forceinline__ int pk_slot_off(int s, int pb) { return s * pb + (s >> 1) * 16; }
-}  // namespace corr2d
-
-template <int K, bool FLIP, bool VEC>
-__global__ __launch_bounds__(256) void k_corr2d_pk(const float* __restrict__ x, float* __restrict__ out, int64_t n0,
-                                                   int64_t n1, const float* __restrict__ w, int ws,
-                                                   const float* __restrict__ b, float beta, int64_t seg, int nstrips,
-                                                   int ntasks) {
-  using Cf = corr2d::PkCfg<K>;
-  constexpr int V = Cf::V, CW = Cf::CW, TW = Cf::TW, TH = Cf::TH, Kc = Cf::Kc, LEFT = Cf::LEFT, NB = Cf::NB;
-  constexpr int WIN = Cf::WIN, PB = Cf::PB, PV = Cf::PV, RS = Cf::RS, NPRE = Cf::NPRE, KP2 = Cf::KP2;
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  unsigned char* ring = smem_raw;
-  float* tl = reinterpret_cast<float*>(smem_raw + Cf::RING_BYTES);  // [K + 1][KP2] tap pairs
-
-  int task = blockIdx.x;
-  {  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
-    const int bb = blockIdx.x, qq = ntasks / 8, rr = ntasks % 8, xcd = bb % 8, kk = bb / 8;
-    task = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + kk;
-  }
-  const int strip = task % nstrips;
-  const int64_t sg = task / nstrips;
-  const int64_t r0 = sg * seg;
-  if (r0 >= n0) return;
-  const int64_t r1 = min(n0, r0 + seg);
-  const int64_t c0 = (int64_t)strip * TW;
-  const int64_t cbase = c0 - LEFT;
-  const int64_t gbase = r0 - Kc;
-  const int nblk = (int)((r1 - r0 + TH - 1) / TH);
-
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int l5 = lane & 31;
-  const int grp = (lane >> 5) * 2 + lane_grp(l5), idx = lane_idx(l5);
-  const int rp = wv * 8 + grp * 2 + (idx >> 3);  // row pair in the block: rows 2 rp, 2 rp + 1
-  const int chunk = idx & 7;
-
-  // taps as pairs (w[q][j], w[q-1][j]), q = 0..K (zero past either end)
-  for (int e = threadIdx.x; e < (K + 2) * KP2; e += 256) {
-    const int q = e / KP2, j = e - q * KP2;
-    const float lo = (q < K && j < K) ? corr2d::tap<float, K, FLIP>(w, ws, q, j) : 0.0f;
-    const float hi = (q >= 1 && q <= K && j < K) ? corr2d::tap<float, K, FLIP>(w, ws, q - 1, j) : 0.0f;
-    tl[2 * e] = lo;
-    tl[2 * e + 1] = hi;
-  }
-  for (int e = threadIdx.x; e < (K - 1) * PV; e += 256) {
-    const int rr = e / PV, cv = e - rr * PV;
-    corr2d::st_lds(reinterpret_cast<float*>(ring + corr2d::pk_slot_off(rr, PB)) + cv * V,
-                   corr2d::load_vec<float, VEC>(x, n0, n1, gbase + rr, cbase + cv * V));
-  }
-  corr2d::V16<float> pre[NPRE];
-  auto issue = [&](int blk) {
-    const int64_t gw0 = (int64_t)blk * TH + (K - 1);
-#pragma unroll
-    for (int m = 0; m < NPRE; ++m) {
-      const int e = threadIdx.x + m * 256;
-      if (e < TH * PV) {
-        const int rr = e / PV, cv = e - rr * PV;
-        pre[m] = corr2d::load_vec<float, VEC>(x, n0, n1, gbase + gw0 + rr, cbase + cv * V);
-      }
-    }
-  };
-  issue(0);
-
-  for (int blk = 0; blk < nblk; ++blk) {
-    {  // land the prefetched rows: window rows blk*TH + K-1 + rr -> ring slot mod RS
-      const int s0 = (int)(((int64_t)blk * TH + (K - 1)) % RS);
-#pragma unroll
-      for (int m = 0; m < NPRE; ++m) {
-        const int e = threadIdx.x + m * 256;
-        if (e < TH * PV) {
-          const int rr = e / PV, cv = e - rr * PV;
-          int s = s0 + rr;
-          if (s >= RS) s -= RS;
-          corr2d::st_lds(reinterpret_cast<float*>(ring + corr2d::pk_slot_off(s, PB)) + cv * V, pre[m]);
-        }
-      }
-    }
-    lds_barrier();
-    if (blk + 1 < nblk) issue(blk + 1);
-
-    const int64_t g = r0 + (int64_t)blk * TH + 2 * rp;  // this thread's first output row
-    if (r0 + (int64_t)blk * TH + wv * 16 < r1) {
-      f2 acc[CW];
-#pragma unroll
-      for (int c = 0; c < CW; ++c) acc[c] = (f2){0.0f, 0.0f};
-      int s = (int)(((int64_t)blk * TH + 2 * rp) % RS);
-      auto rd = [&](float (&dst)[WIN], int slot) {
-        const float* p = reinterpret_cast<const float*>(ring + corr2d::pk_slot_off(slot, PB)) + chunk * CW;
-#pragma unroll
-        for (int t = 0; t < NB; ++t)
-          *reinterpret_cast<corr2d::u32x4*>(dst + t * V) = *reinterpret_cast<const corr2d::u32x4*>(p + t * V);
-      };
-      auto rdt = [&](float (&dst)[2 * KP2], int q) {
-        const float* p = tl + q * 2 * KP2;
-#pragma unroll
-        for (int t = 0; t < 2 * KP2 / V; ++t)
-          *reinterpret_cast<corr2d::u32x4*>(dst + t * V) = *reinterpret_cast<const corr2d::u32x4*>(p + t * V);
-      };
-      auto fmas = [&](const float (&in)[WIN], const float (&h)[2 * KP2]) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const f2 hh = {h[2 * j], h[2 * j + 1]};
-#pragma unroll
-          for (int c = 0; c < CW; ++c) {
-            const float xv = in[LEFT - Kc + c + j];
-            acc[c] = __builtin_elementwise_fma(hh, (f2){xv, xv}, acc[c]);
-          }
-        }
-      };
-      auto keep = [&](const float (&in)[WIN]) {
-#pragma unroll
-        for (int t = 0; t < WIN; ++t)
-          if (t < LEFT - Kc || t >= LEFT + CW + Kc) asm volatile("" ::"v"(in[t]));
-      };
-      auto spread = [&]() {
-        constexpr int NR = NB + 2 * KP2 / V;
-        constexpr int GV = CW * K / (PCS_CORR_SPREAD_DIV * NR);
-        if (PCS_CORR_SPREAD) {
-#pragma unroll
-          for (int t = 0; t < NR; ++t) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x002, GV > 0 ? GV : 1, 0);  // VALU
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      float ia[WIN], ib[WIN], ha[2 * KP2], hb[2 * KP2];
-      rd(ia, s);
-      rdt(ha, 0);
-      // K + 1 input rows (even: K odd), two per trip, the next row read while this one is used
-#pragma unroll 1
-      for (int q = 0; q < K + 1; q += 2) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (++s == RS) s = 0;
-        rd(ib, s);
-        rdt(hb, q + 1);
-        fmas(ia, ha);
-        spread();
-        keep(ib);
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        // the last trip reads one row past the window (a ring row and the spare zero tap row K + 1,
-        // never used): no branch in the loop, so no register copies between the two halves
-        if (++s == RS) s = 0;
-        rd(ia, s);
-        rdt(ha, q + 2);
-        fmas(ib, hb);
-        spread();
-        keep(ia);
-      }
-      // ---- store rows g, g + 1 (optionally + beta * b)
-      const int64_t gc = c0 + chunk * CW;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t gr = g + h;
-        if (gr >= r1) continue;
-        if (VEC) {
-#pragma unroll
-          for (int t = 0; t < CW / V; ++t) {
-            if (gc + t * V < n1) {
-              corr2d::V16<float> o;
-#pragma unroll
-              for (int c = 0; c < V; ++c) o.v[c] = h == 0 ? acc[t * V + c].x : acc[t * V + c].y;
-              if (b) {
-                const corr2d::V16<float> bv = *reinterpret_cast<const corr2d::V16<float>*>(b + gr * n1 + gc + t * V);
-#pragma unroll
-                for (int c = 0; c < V; ++c) o.v[c] = o.v[c] + beta * bv.v[c];
-              }
-              *reinterpret_cast<uint4*>(out + gr * n1 + gc + t * V) = *reinterpret_cast<const uint4*>(o.v);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int c = 0; c < CW; ++c) {
-            if (gc + c < n1) {
-              float o = h == 0 ? acc[c].x : acc[c].y;
-              if (b) o = o + beta * b[gr * n1 + gc + c];
-              out[gr * n1 + gc + c] = o;
-            }
-          }
-        }
-      }
-    }
-    lds_barrier();  // every read of the ring is done before the next landing overwrites it
-  }
-}
-
 namespace corr2d {
 
 // smallest supported odd tier K with K/2 >= every one-sided extent of the PSF
@@ -591,50 +374,6 @@ static int launch(const T* x, T* out, int64_t n0, int64_t n1, const T* w, int ws
   return launch_status();
 }
 
-// the fp32 packed kernel (k_corr2d_pk) only with PCS_CORR_PK=1 (read per call: A/B and tests).  Measured
-// slower than the scalar kernel: 4096^2, k = 15: 0.116-0.119 against 0.108-0.109 ms; k = 31: 0.391-0.404
-// against 0.332-0.340 (3 alternating reps, profiles/r4_corr_pk_ab.txt) -- the FMA issue rate of the
-// scalar kernel is not what bounds it, and the packed form reads twice the tap words per input row
-static bool use_pk() {
-  const char* e = getenv("PCS_CORR_PK");
-  return e != nullptr && atoi(e) != 0;
-}
-
-template <int K, bool FLIP, bool VEC>
-static int slots_pk() {
-  static const int slots = [] {
-    int dev = 0, cus = 256, nb = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_corr2d_pk<K, FLIP, VEC>, 256, PkCfg<K>::LDS_BYTES) !=
-            hipSuccess ||
-        nb < 1)
-      nb = 1;
-    return cus * nb;
-  }();
-  return slots;
-}
-
-template <int K, bool FLIP, bool VEC>
-static int launch_pk(const float* x, float* out, int64_t n0, int64_t n1, const float* w, int ws, const float* b,
-                     float beta, hipStream_t st) {
-  using Cf = PkCfg<K>;
-  const int64_t nstrips = (n1 + Cf::TW - 1) / Cf::TW;
-  const int64_t slots = slots_pk<K, FLIP, VEC>();
-  int64_t segs = slots / nstrips;
-  if (segs < 1) segs = 1;
-  int64_t seg = (n0 + segs - 1) / segs;
-  const int64_t min_seg = Cf::TH / 2;
-  if (seg < min_seg) seg = min_seg;
-  seg = (seg + 7) / 8 * 8;
-  segs = (n0 + seg - 1) / seg;
-  const int64_t ntasks = nstrips * segs;
-  if (ntasks > 0x7fffffff) return PCS_EUNSUPPORTED;
-  k_corr2d_pk<K, FLIP, VEC><<<(unsigned)ntasks, 256, Cf::LDS_BYTES, st>>>(x, out, n0, n1, w, ws, b, beta, seg,
-                                                                          (int)nstrips, (int)ntasks);
-  return launch_status();
-}
-
 template <typename T, bool FLIP>
 static int dispatch(int K, const void* x, void* out, int64_t n0, int64_t n1, const void* w, int ws, const void* b,
                     double beta, hipStream_t st) {
@@ -645,26 +384,6 @@ static int dispatch(int K, const void* x, void* out, int64_t n0, int64_t n1, con
   const T* ww = (const T*)w;
   const T* bb = (const T*)b;
   const T be = (T)beta;
-  if constexpr (sizeof(T) == 4) {
-    if (use_pk()) {
-#define PCS_CORR_PK_CASE(KK)                                                               \
-  case KK:                                                                                 \
-    return vec ? launch_pk<KK, FLIP, true>(xx, oo, n0, n1, ww, ws, bb, be, st)          \
-               : launch_pk<KK, FLIP, false>(xx, oo, n0, n1, ww, ws, bb, be, st);
-      switch (K) {
-        PCS_CORR_PK_CASE(3)
-        PCS_CORR_PK_CASE(5)
-        PCS_CORR_PK_CASE(7)
-        PCS_CORR_PK_CASE(9)
-        PCS_CORR_PK_CASE(11)
-        PCS_CORR_PK_CASE(13)
-        PCS_CORR_PK_CASE(15)
-        PCS_CORR_PK_CASE(31)
-        default: return PCS_EUNSUPPORTED;
-      }
-#undef PCS_CORR_PK_CASE
-    }
-  }
 #define PCS_CORR_CASE(KK)                                                                  \
   case KK:                                                                                 \
     return vec ? launch<T, KK, FLIP, true>(xx, oo, n0, n1, ww, ws, bb, be, st)          \

@@ -8,10 +8,8 @@
 // with F = 1/2 ||Conv x - y||^2 (Conv separable, centred taps), 1/2 ||x - y||^2, 0, or a
 // precomputed gradient buffer; K = Gradient(kind='forward'); H = lam*L1 / lam*L21 (pixel
 // groups); G = Null / NonNegativeOrthant / Segment.  The tile kernel is in pds_tile.hpp.
-#include "pds_march.hpp"
-#include "pds_nmarch.hpp"
+#include "pds_host.hpp"
 #include "pds_pt.hpp"
-#include "pds_smarch.hpp"
 
 namespace pcs {
 
@@ -80,59 +78,7 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_finalize(const double* _
   if (threadIdx.x == 0) finalize_from(v, c, hist);
 }
 
-// ---------------------------------------------------------------- host dispatch
-template <typename T>
-struct Tile {
-  static constexpr int TH = 31;  // U region = 32 rows
-  static constexpr int NT = 256;
-};
-template <>
-struct Tile<double> {
-  static constexpr int TH = 15;
-  static constexpr int NT = 256;
-};
-
-static int tier_for(int half) {
-  if (half <= 3) return 3;
-  if (half <= 7) return 7;
-  if (half <= 11) return 11;
-  if (half <= 15) return 15;
-  return -1;
-}
-
-static bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
-
-static Slab make_slab(const pcs_pds2d_args* a) {
-  const int vec = (a->n1 % 4 == 0) && aligned16(a->x) && aligned16(a->xn) && aligned16(a->z) && aligned16(a->zn) &&
-                  aligned16(a->y) && aligned16(a->gbuf);
-  return Slab{a->n0, a->n1, a->row0, a->rows, a->halo_x, a->halo_y, a->halo_z, vec};
-}
-
-template <typename T>
-static Params<T> make_params(const pcs_pds2d_args* a) {
-  Params<T> P;
-  P.tau = (T)a->tau;
-  P.sigma = (T)a->sigma;
-  P.inv_sigma = (T)(1.0 / a->sigma);
-  P.rho = (T)a->rho;
-  P.omr = (T)(1.0 - a->rho);
-  const double t_h = (1.0 / a->sigma) * a->lam;  // ProxFuncPostComp: tau*scale with tau = 1/sigma
-  P.t_h = (T)t_h;
-  P.inv_t_h = (T)(1.0 / t_h);
-  P.lam = (T)a->lam;
-  P.inv_step0 = (T)(1.0 / a->step0);
-  P.inv_step1 = (T)(1.0 / a->step1);
-  P.unit0 = a->step0 == 1.0;
-  P.unit1 = a->step1 == 1.0;
-  P.seg_a = (T)a->seg_a;
-  P.seg_b = (T)a->seg_b;
-  return P;
-}
-
-static RedOut red_out(const pcs_pds2d_args* a) {
-  return a->hist ? RedOut{nullptr, nullptr, 0} : RedOut{a->sums_out, a->pre_partials, (int)a->n_pre};
-}
-
+// ---------------------------------------------------------------- host dispatch (planning: pds_host.hpp)
 template <typename T, int FK, int H>
 static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   constexpr int TH = Tile<T>::TH, NT = Tile<T>::NT;
@@ -147,170 +93,6 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
       (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
       tiles_x, (int)ntiles, tiles_x, 0);
   return launch_status();
-}
-
-// ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel (pds_march.hpp) on every
-// 64-column strip, reduction + loop control in its last workgroups
-constexpr int kMarchNT = 256;
-constexpr int kNMarchNT = 256;
-
-struct MarchPlan {
-  int tiles_x;  // 64-column strips
-  Bands bd;     // row segments of the launch's bands
-  int ntasks;   // strips x segments
-};
-
-// own-row bands [ra0, rb0) and [ra1, rb1) of a launch (0 <= ra0 <= rb0 <= ra1 <= rb1 <= rows)
-struct RowBands {
-  int64_t ra0, rb0, ra1, rb1;
-};
-static RowBands full_bands(const pcs_pds2d_args* a) { return RowBands{0, a->rows, a->rows, a->rows}; }
-
-// Segments of TS-row steps over the bands: about `slots / tiles_x` segments in all (one wave of
-// resident workgroups), at least one per non-empty band, at most one per `min_steps` steps.
-static void plan_bands(RowBands rb, int TS, int tiles_x, int slots, int min_steps, MarchPlan* p) {
-  if (rb.rb0 == rb.ra0) rb = RowBands{rb.ra1, rb.rb1, rb.rb1, rb.rb1};
-  const int64_t L0 = rb.rb0 - rb.ra0, L1 = rb.rb1 - rb.ra1;
-  const int64_t steps = (L0 + TS - 1) / TS + (L1 + TS - 1) / TS;
-  const int64_t bands = (L0 > 0) + (L1 > 0);
-  int64_t nseg = slots / tiles_x;
-  const int64_t max_seg = (steps + min_steps - 1) / min_steps;
-  nseg = nseg > max_seg ? max_seg : nseg;
-  nseg = nseg < bands ? bands : nseg;
-  nseg = nseg < 1 ? 1 : nseg;
-  const int64_t seg_len = ((steps + nseg - 1) / nseg) * TS;
-  const int64_t n0 = (L0 + seg_len - 1) / seg_len, n1 = (L1 + seg_len - 1) / seg_len;
-  p->tiles_x = tiles_x;
-  p->bd = Bands{(int)seg_len, (int)n0, (int)rb.ra0, (int)rb.rb0, (int)rb.ra1, (int)rb.rb1};
-  p->ntasks = (int)(tiles_x * (n0 + n1));
-}
-
-// resident workgroups of the march kernel on the whole device (queried once)
-template <int H>
-static int march_slots() {
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess || cus < 1)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_march<float, H, PCS_H_L21, kMarchNT>, kMarchNT,
-                                                     0) != hipSuccess ||
-        nb < 1)
-      nb = 3;
-    (void)hipGetLastError();
-    slots = cus * nb;
-  }
-  return slots;
-}
-
-// One march task = one 64-column strip x one row segment; as many segments as fill the
-// device in one wave of resident workgroups.  False for narrow images (the tile kernel).
-template <int H>
-static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p);
-
-// the normal-operator march kernel (pds_nmarch.hpp): fp32 separable tiers 3 / 7 with the host's
-// Conv^T y and N tables; images of at least 64 x 64 (the edge bands of N never overlap).  Backward /
-// centred K too (its GEN geometry) unless PCS_NMARCH_GEN=0, when the last strip keeps its column
-// c0 - 1 out of N_h's right edge band (n1 - c0_last > H); else those K take the stencil march
-static bool nmarch_gen_enabled() {
-  const char* e = getenv("PCS_NMARCH_GEN");  // read per call (tests and the A/B switch it)
-  return e == nullptr || atoi(e) != 0;
-}
-static bool use_nmarch(const pcs_pds2d_args* a) {
-  if (!(a->cty != nullptr && a->ntaps != nullptr && aligned16(a->cty) && a->n0 >= 64 && a->n1 >= 64)) return false;
-  if (a->kkind == PCS_K_GRAD_FORWARD) return true;
-  if (a->kkind != PCS_K_GRAD_BACKWARD && a->kkind != PCS_K_GRAD_CENTERED) return false;
-  const int64_t last = a->n1 - 64 * ((a->n1 + 63) / 64 - 1);  // width of the last 64-column strip
-  return nmarch_gen_enabled() && last > tier_for(a->half);
-}
-
-template <int H>
-static int nmarch_slots(bool gen) {
-  static int slots_f = 0, slots_g = 0;
-  int& slots = gen ? slots_g : slots_f;
-  if (slots == 0) {
-    int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess || cus < 1)
-      cus = 256;
-    const hipError_t oe =
-        gen ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                  &nb, k_pds2d_nmarch_gen<float, H, PCS_H_L21, kNMarchNT, PCS_CENTERED>, kNMarchNT, 0)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_nmarch<float, H, PCS_H_L21, kNMarchNT>,
-                                                           kNMarchNT, 0);
-    if (oe != hipSuccess ||
-        nb < 1)
-      nb = 3;
-    (void)hipGetLastError();
-    slots = cus * nb;
-    const char* e = getenv("PCS_NMARCH_SLOTS");  // diagnostics: grid-size sweep
-    if (e && atoi(e) > 0) slots = atoi(e);
-  }
-  return slots;
-}
-
-template <int H>
-static bool march_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
-  const bool nm = use_nmarch(a);
-  const int tw = nm ? NMarch<H>::TW : March<H>::TW;
-  const int tiles_x = (int)((a->n1 + tw - 1) / tw);
-  if (tiles_x < 2) return false;
-  plan_bands(rb, March<H>::TS, tiles_x, nm ? nmarch_slots<H>(a->kkind != PCS_K_GRAD_FORWARD) : march_slots<H>(), 1, p);
-  return true;
-}
-
-static bool use_march(const pcs_pds2d_args* a) {
-  static int disabled = -1;  // PCS_NO_MARCH=1: diagnostics, force the tile kernel
-  if (disabled < 0) disabled = getenv("PCS_NO_MARCH") != nullptr;
-  if (disabled) return false;
-  const int t = tier_for(a->half);
-  if (a->dtype != PCS_F32 || a->fkind != PCS_F_SEPCONV || (t != 3 && t != 7) || !make_slab(a).vec) return false;
-  if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return false;
-  if (a->kkind != PCS_K_GRAD_FORWARD && !use_nmarch(a)) return false;  // only the normal-operator march is general
-  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
-                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
-  // 32-bit indexing and buffer views of at most 2^30 bytes (pds_march.hpp kOOB)
-  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 4 <= (1LL << 30))) return false;
-  MarchPlan p;
-  return t == 3 ? march_plan<3>(a, full_bands(a), &p) : march_plan<7>(a, full_bands(a), &p);
-}
-
-template <int H, int HK>
-static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  MarchPlan p;
-  if (!march_plan<H>(a, rb, &p)) return PCS_EINVAL;
-  if (p.ntasks == 0) return PCS_OK;
-  const Slab s64 = make_slab(a);
-  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
-  const Params<float> P = make_params<float>(a);
-  if (use_nmarch(a) && a->kkind != PCS_K_GRAD_FORWARD) {
-    auto kern = a->kkind == PCS_K_GRAD_BACKWARD ? k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_BACKWARD>
-                                                : k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_CENTERED>;
-    kern<<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn,
-                                                   (const float*)a->cty, (const float*)a->ntaps, s, P, a->gkind,
-                                                   a->edge, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
-                                                   p.tiles_x, p.bd, p.ntasks);
-    return launch_status();
-  }
-  if (use_nmarch(a)) {
-    k_pds2d_nmarch<float, H, HK, kNMarchNT><<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>(
-        (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->cty,
-        (const float*)a->ntaps, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x,
-        p.bd, p.ntasks);
-    return launch_status();
-  }
-  if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
-  k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
-      (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
-      (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
-      a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);
-  return launch_status();
-}
-
-template <int H>
-static int launch_march(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  return a->hkind == PCS_H_L21 ? launch_march<H, PCS_H_L21>(a, rb, st) : launch_march<H, PCS_H_L1>(a, rb, st);
 }
 
 // ---- fp32 pointwise grad F (NULL / DENOISE / GRADBUF): the row-marching kernel of pds_pt.hpp
@@ -376,268 +158,15 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb);
 
-// persistent form: all n iterations in one launch; the grid must be co-resident
-template <int FK, int HK>
-static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hipStream_t st) {
-  int dev = 0, cus = 0, nb = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pds2d_pt_loop<FK, HK>, 256, 0) != hipSuccess)
-    return PCS_ELAUNCH;
-  const int tiles_x = (int)((a->n1 + PtGeom::TW - 1) / PtGeom::TW);
-  // the occupancy query can over-report by one block/CU for SGPR-heavy kernels: at most 4
-  // blocks of 256 threads per CU for a grid that must be co-resident
-  nb = nb > 3 ? 3 : nb;  // and 3 per CU is the fastest grid of the per-launch kernel too
-  if (tiles_x < 2 || nb < 1) return PCS_EUNSUPPORTED;
-  // one wave of this kernel's resident workgroups, and never more tasks than the per-launch
-  // plan that sized the caller's partials / ws buffers (pcs_pds2d_nblocks, pt_slots())
-  const int slots = cus * nb < pt_slots() ? cus * nb : pt_slots();
-  MarchPlan p;
-  plan_bands(full_bands(a), PtGeom::TS, tiles_x, slots, 4, &p);
-  if (p.ntasks < 1 || (int64_t)p.ntasks > (int64_t)cus * nb || (int64_t)p.ntasks > bands_nblocks(a, full_bands(a)))
-    return PCS_EUNSUPPORTED;
-  // fresh barrier state for every launch: a timed-out barrier of an earlier launch (sticky
-  // flag, stranded arrival count) cannot leak into this one
-  if (hipMemsetAsync(bar, 0, (size_t)pcs_grid_bar_bytes(), st) != hipSuccess) return PCS_ELAUNCH;
-  const Slab s64 = make_slab(a);
-  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
-  const Params<float> P = make_params<float>(a);
-  const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
-  k_pds2d_pt_loop<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>(
-      (float*)a->x, (float*)a->xn, (float*)a->z, (float*)a->zn, g, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl,
-      a->hist, a->ws, bar, (int)n, p.tiles_x, p.bd, p.ntasks);
-  return launch_status();
-}
-
-template <int FK>
-static int launch_pt_loop(const pcs_pds2d_args* a, int64_t n, unsigned* bar, hipStream_t st) {
-  return a->hkind == PCS_H_L21 ? launch_pt_loop<FK, PCS_H_L21>(a, n, bar, st)
-                               : launch_pt_loop<FK, PCS_H_L1>(a, n, bar, st);
-}
-
 template <int FK>
 static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   return a->hkind == PCS_H_L21 ? launch_pt<FK, PCS_H_L21>(a, rb, st) : launch_pt<FK, PCS_H_L1>(a, rb, st);
 }
 
-// ---- fp32 general-stencil K (backward / centred Gradient, Laplacian) with a pointwise grad F:
-// the row-marching kernel of pds_smarch.hpp (PCS_SM_FWD=1 also routes the forward Gradient
-// through it: diagnostics / A-B against pds_pt.hpp)
-static bool sm_forward() {
-  const char* e = getenv("PCS_SM_FWD");  // read per call (tests switch it)
-  return e != nullptr && atoi(e) != 0;
-}
-
-// 16-row halves per step of the march (SMarch RS): 2 = 32-row steps (twice the loads in flight per
-// barrier, half the steps; the Laplacian's single z component leaves the LDS for 64-row rings at 3
-// workgroups / CU).  Measured (tools/sm_probe.py, profiles/r4_sm_rs_ab.txt): Laplacian 2048^2 28.7 us
-// either way, 4096^2 82.0 against 76.6 us; centred 31.0 against 29.6-29.9 us at 2048^2 -- the 2048^2
-// time is not the per-step latency.  Default 1; PCS_SM_RS=2 (read once) for every fp32 K (parity
-// green at RS = 2 for every smarch case, profiles/r4_sm_rs_ab.txt)
-static int sm_rs(const pcs_pds2d_args* a) {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("PCS_SM_RS");
-    env = e ? atoi(e) : 0;
-  }
-  if (a->dtype != PCS_F32) return 1;
-  return env == 2 ? 2 : 1;
-}
-
-// resident workgroups (<= 3 per CU: fewer, longer row segments, as the pt kernel), queried once per
-// kernel shape: RS = 1 takes the centred-K kernel's occupancy for every K (rings of the same size or
-// smaller), RS = 2 its own K's
-template <typename T, int KK, int RS>
-static int sm_slots() {
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                hipSuccess || cus < 1)
-      cus = 256;
-    constexpr int QK = RS == 1 ? PCS_CENTERED : KK;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, k_pds2d_smarch<T, QK, PCS_F_DENOISE, QK == SK_LAP ? PCS_H_L1 : PCS_H_L21, RS>, 256, 0) != hipSuccess ||
-        nb < 1)
-      nb = sizeof(T) == 4 ? 3 : 2;
-    (void)hipGetLastError();
-    slots = cus * (nb < 3 ? nb : 3);
-    // fp64: three rounds of the resident workgroups (later ones start as earlier ones finish), with
-    // segments of >= 8 steps (sm_plan).  fp64 C3 4096^2: 3326-3379 it/s against 3194-3219 at one round,
-    // 3139-3226 at four or six (profiles/r4_f64_step_slots.txt)
-    if (sizeof(T) == 8) slots *= 3;
-    const char* e = getenv("PCS_SM_SLOTS");  // diagnostics: grid-size sweep
-    if (e && atoi(e) > 0) slots = atoi(e);
-  }
-  return slots;
-}
-
-static int sm_slots_for(const pcs_pds2d_args* a, int rs) {
-  if (a->dtype == PCS_F64) return sm_slots<double, PCS_CENTERED, 1>();
-  if (rs == 1) return sm_slots<float, PCS_CENTERED, 1>();
-  switch (a->kkind) {
-    case PCS_K_GRAD_FORWARD: return sm_slots<float, PCS_FORWARD, 2>();
-    case PCS_K_GRAD_BACKWARD: return sm_slots<float, PCS_BACKWARD, 2>();
-    case PCS_K_LAPLACIAN: return sm_slots<float, SK_LAP, 2>();
-    default: return sm_slots<float, PCS_CENTERED, 2>();
-  }
-}
-
-static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
-  const int tiles_x = (int)((a->n1 + 63) / 64);
-  if (tiles_x < 2) return false;
-  const int rs = sm_rs(a);
-  // at least 4 16-row halves per segment (2 steps of 32 rows); fp64 at least 8 steps
-  plan_bands(rb, 16 * rs, tiles_x, sm_slots_for(a, rs), a->dtype == PCS_F64 ? 8 : 4 / rs, p);
-  return true;
-}
-
-// F = (1/2)||Conv x - y||^2, Conv separable, with a non-forward K: grad F = N x - Conv^T y, N x by the
-// in-plane normal-operator kernel into gbuf (pcs_conv2d_sep_ata_planes on the whole image: two
-// composite-tap passes), then the march step reads gbuf and cty -- whole images only
-// local rows [lo, hi) of the stored window (halo h) clipped to the image
-static void window_rows(const pcs_pds2d_args* a, int h, int64_t* lo, int64_t* hi) {
-  *lo = -h > -a->row0 ? -h : -a->row0;
-  *hi = a->rows + h < a->n0 - a->row0 ? a->rows + h : a->n0 - a->row0;
-}
-
-static bool sm_normal(const pcs_pds2d_args* a) {
-  if (a->fkind != PCS_F_SEPCONV || !a->cty || !a->gbuf || !aligned16(a->cty) || a->halo_y != a->halo_x) return false;
-  if (a->half < 0 || a->half > 7 || !a->taps0 || !a->taps1) return false;
-  int64_t lo, hi;
-  window_rows(a, a->halo_x, &lo, &hi);
-  // shape / tap validation only (nplanes 0): any non-null input will do before x is bound
-  return pcs_conv2d_sep_ata_planes(a->dtype, a->x ? a->x : a->cty, const_cast<void*>(a->gbuf), 0, hi - lo, a->n1,
-                                   a->taps0, 2 * a->half + 1, a->half, a->taps1, 2 * a->half + 1, a->half,
-                                   nullptr) == PCS_OK;
-}
-
-static bool use_march(const pcs_pds2d_args* a);
-// sep_ata.hip: N x - sub by the two-pass normal-operator kernel (PCS_EUNSUPPORTED: taps / layout it does not take)
-int sep_normal_minus(int dt, const void* in, void* out, const void* sub, int64_t np, int64_t n1, int64_t n2,
-                     const void* ha, int ka, int offa, const void* hb, int kb, int offb, hipStream_t st);
-
-// fp64 (the reference's default dtype): every K kind, the forward Gradient included, takes this march
-// (the forward-only fp32 kernels pds_pt.hpp / pds_nmarch.hpp have no fp64 form)
-static bool use_smarch(const pcs_pds2d_args* a) {
-  if (a->kkind == PCS_K_GRAD_FORWARD && !sm_forward() && a->dtype != PCS_F64 && a->mkind == PCS_M_NONE) return false;
-  // separable PSF with backward / centred K: the fused normal-operator march (one launch) when it applies
-  if (a->kkind != PCS_K_GRAD_FORWARD && a->fkind == PCS_F_SEPCONV && use_march(a)) return false;
-  if (a->kkind < PCS_K_GRAD_FORWARD || a->kkind > PCS_K_LAPLACIAN) return false;
-  if ((a->dtype != PCS_F32 && a->dtype != PCS_F64) || !make_slab(a).vec) return false;
-  if (a->fkind != PCS_F_NULL && a->fkind != PCS_F_DENOISE && a->fkind != PCS_F_GRADBUF &&
-      !((a->kkind != PCS_K_GRAD_FORWARD || a->dtype == PCS_F64) && sm_normal(a)))
-    return false;
-  if (a->mkind != PCS_M_NONE && (a->fkind != PCS_F_NULL || !aligned16(a->ym) || !aligned16(a->zm) || !aligned16(a->zmn)))
-    return false;
-  if (a->hkind != PCS_H_L1 && (a->hkind != PCS_H_L21 || a->kkind == PCS_K_LAPLACIAN)) return false;
-  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
-                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
-  const int64_t esz = a->dtype == PCS_F64 ? 8 : 4;
-  // 32-bit indexing; every buffer view (z: one per component) at most 2^30 bytes (kOOB)
-  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * esz <= (1LL << 30))) return false;
-  MarchPlan p;
-  return sm_plan(a, full_bands(a), &p);
-}
-
-template <typename T>
-static SParamsT<T> make_sparams(const pcs_pds2d_args* a) {
-  SParamsT<T> Q;
-  Q.ih20 = (T)(1.0 / (a->step0 * a->step0));
-  Q.ih21 = (T)(1.0 / (a->step1 * a->step1));
-  Q.w0 = (T)a->w0;
-  Q.w1 = (T)a->w1;
-  Q.edge = a->edge != 0;
-  return Q;
-}
-
-template <typename T, int KK, int FK, int HK>
-static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  MarchPlan p;
-  if (!sm_plan(a, rb, &p)) return PCS_EINVAL;
-  if (p.ntasks == 0) return PCS_OK;
-  const Slab s64 = make_slab(a);
-  const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
-  const Params<T> P = make_params<T>(a);
-  const T* g = FK == PCS_F_DENOISE                       ? (const T*)a->y
-               : (FK == PCS_F_GRADBUF || FK == SM_F_NB) ? (const T*)a->gbuf
-                                                        : nullptr;
-  const T* b = FK == SM_F_NB ? (const T*)a->cty : nullptr;
-  if constexpr (FK == SM_F_MASK) g = (const T*)a->ym;
-  const T* mi = FK == SM_F_MASK ? (const T*)a->zm : nullptr;
-  T* mo = FK == SM_F_MASK ? (T*)a->zmn : nullptr;
-  auto* kern = k_pds2d_smarch<T, KK, FK, HK, 1>;
-  if constexpr (sizeof(T) == 4)
-    if (sm_rs(a) == 2) kern = k_pds2d_smarch<T, KK, FK, HK, 2>;
-  kern<<<(unsigned)p.ntasks, 256, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, mi, mo, s, P,
-                                           make_sparams<T>(a), a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws,
-                                           red_out(a), p.tiles_x, p.bd, p.ntasks);
-  return launch_status();
-}
-
-template <typename T, int KK, int FK>
-static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  if constexpr (KK == SK_LAP) return launch_smarch<T, KK, FK, PCS_H_L1>(a, rb, st);
-  else
-    return a->hkind == PCS_H_L21 ? launch_smarch<T, KK, FK, PCS_H_L21>(a, rb, st)
-                                 : launch_smarch<T, KK, FK, PCS_H_L1>(a, rb, st);
-}
-
-template <typename T, int KK>
-static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  if (a->fkind == PCS_F_SEPCONV) {  // N x -> gbuf on the stored rows (clipped to the image), then the
-    // step with grad F = gbuf - cty; whole slabs only (the N x pass runs once per iteration).  The
-    // forward Gradient comes here in fp64 only (fp32 has the fused normal-operator march)
-    if ((KK == PCS_FORWARD && sizeof(T) == 4) || rb.ra0 != 0 || rb.rb0 != a->rows) return PCS_EUNSUPPORTED;
-    int64_t lo, hi;
-    window_rows(a, a->halo_x, &lo, &hi);
-    const int64_t off = (lo + a->halo_x) * a->n1;
-    // grad F = N x - Conv^T y formed by the normal-operator kernel itself (it reads Conv^T y as it stores): the
-    // step then reads one buffer (7 words instead of 8; the same subtraction, bit for bit).  PCS_NX_SUB=0
-    // (read once): N x alone and the subtraction in the step
-    static int nx_sub = -1;
-    if (nx_sub < 0) {
-      const char* e = getenv("PCS_NX_SUB");
-      nx_sub = e == nullptr || atoi(e) != 0;
-    }
-    if (nx_sub) {
-      const int rs = sep_normal_minus(a->dtype, (const T*)a->x + off, (T*)const_cast<void*>(a->gbuf) + off,
-                                      (const T*)a->cty + off, 1, hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half,
-                                      a->taps1, 2 * a->half + 1, a->half, st);
-      if (rs == PCS_OK) return launch_smarch<T, KK, PCS_F_GRADBUF>(a, rb, st);
-      if (rs != PCS_EUNSUPPORTED) return rs;
-    }
-    const int rc = pcs_conv2d_sep_ata_planes(a->dtype, (const T*)a->x + off, (T*)const_cast<void*>(a->gbuf) + off, 1,
-                                             hi - lo, a->n1, a->taps0, 2 * a->half + 1, a->half, a->taps1,
-                                             2 * a->half + 1, a->half, st);
-    if (rc != PCS_OK) return rc;
-    return launch_smarch<T, KK, SM_F_NB>(a, rb, st);
-  }
-  if (a->mkind == PCS_M_L1LOSS) return launch_smarch<T, KK, SM_F_MASK>(a, rb, st);
-  if (a->fkind == PCS_F_DENOISE) return launch_smarch<T, KK, PCS_F_DENOISE>(a, rb, st);
-  if (a->fkind == PCS_F_GRADBUF) return launch_smarch<T, KK, PCS_F_GRADBUF>(a, rb, st);
-  return launch_smarch<T, KK, PCS_F_NULL>(a, rb, st);
-}
-
-template <typename T>
-static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  switch (a->kkind) {
-    case PCS_K_GRAD_FORWARD: return launch_smarch<T, PCS_FORWARD>(a, rb, st);
-    case PCS_K_GRAD_BACKWARD: return launch_smarch<T, PCS_BACKWARD>(a, rb, st);
-    case PCS_K_GRAD_CENTERED: return launch_smarch<T, PCS_CENTERED>(a, rb, st);
-    case PCS_K_LAPLACIAN: return launch_smarch<T, SK_LAP>(a, rb, st);
-    default: return PCS_EINVAL;
-  }
-}
-
-static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  return a->dtype == PCS_F64 ? launch_smarch<double>(a, rb, st) : launch_smarch<float>(a, rb, st);
-}
-
 // the row-marching families (march, pt, smarch) take row bands; the tile kernel runs whole slabs only
 static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
-  if (use_smarch(a)) return launch_smarch(a, rb, st);
-  if (use_march(a)) return tier_for(a->half) == 3 ? launch_march<3>(a, rb, st) : launch_march<7>(a, rb, st);
+  if (use_smarch(a)) return a->dtype == PCS_F64 ? sm_launch<double>(a, rb, st) : sm_launch<float>(a, rb, st);
+  if (use_march(a)) return launch_march(a, rb, st);
   if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (a->fkind == PCS_F_DENOISE) return launch_pt<PCS_F_DENOISE>(a, rb, st);
   if (a->fkind == PCS_F_GRADBUF) return launch_pt<PCS_F_GRADBUF>(a, rb, st);
@@ -846,25 +375,6 @@ int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t st) {
   }
   return PCS_OK;
 }
-
-// The same n iterations as pcs_pds2d_run in ONE launch of the pointwise-F row-marching kernel
-// (fp32 NULL / DENOISE / GRADBUF families), a grid barrier per iteration in place of the
-// kernel boundary.  `bar`: pcs_grid_bar_bytes() device bytes, zeroed once before first use.
-// PCS_EUNSUPPORTED when the problem is not of that family or its grid is not co-resident.
-int pcs_pds2d_run_persistent(const pcs_pds2d_args* a, int64_t n, void* bar, hipStream_t st) {
-  if (!a || n < 0 || n > 0x7fffffff || !a->hist || !bar || !aligned16(bar)) return PCS_EINVAL;
-  const int rc = check_args(a);
-  if (rc != PCS_OK) return rc;
-  if (a->rows != a->n0 || a->kkind != PCS_K_GRAD_FORWARD || use_smarch(a) || use_march(a) || !use_pt(a))
-    return PCS_EUNSUPPORTED;
-  if (n == 0) return PCS_OK;
-  unsigned* b = (unsigned*)bar;
-  if (a->fkind == PCS_F_DENOISE) return launch_pt_loop<PCS_F_DENOISE>(a, n, b, st);
-  if (a->fkind == PCS_F_GRADBUF) return launch_pt_loop<PCS_F_GRADBUF>(a, n, b, st);
-  return launch_pt_loop<PCS_F_NULL>(a, n, b, st);
-}
-
-int64_t pcs_grid_bar_bytes(void) { return 512; }
 
 int64_t pcs_ctrl_bytes(void) { return 64; }
 

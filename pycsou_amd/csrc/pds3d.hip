@@ -157,11 +157,8 @@ constexpr int k3C0K = 15;
 #ifndef PCS_3D_RPD
 #define PCS_3D_RPD 1
 #endif
-// ring voxels 0 and 1 of a ring thread as one packed pair (v_pk_fma_f32 with the tap broadcast, 64-bit
-// ring shifts), voxel 2 scalar; the same fma chains per voxel.  Diagnostics (A/B)
-#ifndef PCS_3D_PK
-#define PCS_3D_PK 0
-#endif
+// (a packed-pair form of the rings -- v_pk_fma_f32 on voxels 0 and 1 -- measured 529 against 611 it/s on
+// C4, profiles/r4_c4_packed_ring_ab.txt: removed in round 5)
 
 template <typename T, int FK, bool VEC>
 // minimum resident workgroups per CU the register budget targets (non-fold kernels; diagnostics knob):
@@ -247,16 +244,12 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
 #pragma unroll
   for (int m = 0; m < RV; ++m) roff[m] = inplane<T>(v, r1 + rrow, c2 + rcol + m);
   T h0[KR], tw[KR][RV], rw[KR][RV], tq[RV], wq[RV];
-  constexpr bool PK = FOLD && PCS_3D_PK && RV == 3 && std::is_same<T, float>::value;
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  f2v tp[PK ? KR : 1], rp[PK ? KR : 1];  // PK: voxels 0, 1 (tw / rw keep voxel 2)
   if constexpr (FOLD) {
 #pragma unroll
     for (int j = 0; j < KR; ++j) {
       h0[j] = j < k0 ? taps0[j] : T(0);
 #pragma unroll
       for (int m = 0; m < RV; ++m) tw[j][m] = rw[j][m] = T(0);
-      if constexpr (PK) tp[j] = rp[j] = f2v{0.f, 0.f};
     }
   }
   auto load0 = [&](int Pl, T (&tv)[RV], T (&wv)[RV]) {  // t of plane Pl, w of plane Pl - off0
@@ -271,44 +264,6 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
   // o = g(Pl - KR + 1) = sum_j h0[KR-1-j] r(Pl - off0 - j) (the adjoint's flipped taps): the sums
   // of k_conv0_rta for 15 taps in its order
   auto push0 = [&](int Pl, const T (&tv)[RV], const T (&wv)[RV], T (&o)[RV]) {
-    if constexpr (PK) {
-#pragma unroll
-      for (int j = 0; j + 1 < KR; ++j) {
-        tp[j] = tp[j + 1];
-        tw[j][2] = tw[j + 1][2];
-      }
-      tp[KR - 1] = f2v{tv[0], tv[1]};
-      tw[KR - 1][2] = tv[2];
-      const int pr = Pl - off0, gpr = v.plane0 + pr;
-      const bool rv = gpr >= 0 && gpr < v.n0 && pr >= -v.hg && pr < v.planes + v.hg;
-      f2v acc2 = {0.f, 0.f};
-      T acc1 = T(0);
-#pragma unroll
-      for (int j = 0; j < KR; ++j) {
-        acc2 = __builtin_elementwise_fma(f2v{h0[j], h0[j]}, tp[KR - 1 - j], acc2);
-        acc1 = __builtin_fmaf(h0[j], tw[KR - 1 - j][2], acc1);
-      }
-#pragma unroll
-      for (int j = 0; j + 1 < KR; ++j) {
-        rp[j] = rp[j + 1];
-        rw[j][2] = rw[j + 1][2];
-      }
-      const f2v rm2 = acc2 - f2v{wv[0], wv[1]};
-      const T rm1 = acc1 - wv[2];
-      rp[KR - 1] = rv ? rm2 : f2v{0.f, 0.f};
-      rw[KR - 1][2] = rv ? rm1 : T(0);
-      f2v s2 = {0.f, 0.f};
-      T s1 = T(0);
-#pragma unroll
-      for (int j = 0; j < KR; ++j) {
-        s2 = __builtin_elementwise_fma(f2v{h0[KR - 1 - j], h0[KR - 1 - j]}, rp[KR - 1 - j], s2);
-        s1 = __builtin_fmaf(h0[KR - 1 - j], rw[KR - 1 - j][2], s1);
-      }
-      o[0] = s2.x;
-      o[1] = s2.y;
-      o[2] = s1;
-      return;
-    }
 #pragma unroll
     for (int j = 0; j + 1 < KR; ++j)
 #pragma unroll

@@ -162,43 +162,4 @@ __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], dou
   }
 }
 
-// ---- grid barrier of the persistent multi-iteration launch (every workgroup co-resident,
-// checked on the host).  Layout (pcs_grid_bar_bytes): [0] arrival counter, [32] generation,
-// [64] timeout flag.  Each wave drains its stores, thread 0 releases at agent scope (L2
-// write-back: the other XCDs read these rows next iteration), the last arriver bumps the
-// generation, the others spin on it and acquire (L2 invalidate), as a kernel boundary does.
-// A bounded spin (~seconds) turns a non-resident grid into an error instead of a hang.
-constexpr unsigned kBarSpin = 1u << 22;
-
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nblocks, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* gen = bar + 32;
-    const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait can be dropped (ROCm 7.2)
-    int ok = 1;
-    if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned n = 0;
-      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        if (++n == kBarSpin) {
-          ok = 0;
-          __hip_atomic_store(bar + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // invalidate complete before the barrier
-    flag[1] = ok && __hip_atomic_load(bar + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-  }
-  __syncthreads();
-  return flag[1] != 0;
-}
-
 }  // namespace pcs

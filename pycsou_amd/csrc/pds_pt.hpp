@@ -288,41 +288,4 @@ __global__ __launch_bounds__(256) void k_pds2d_pt(const float* __restrict__ x, f
   }
 }
 
-// Persistent form: `niter` iterations in one launch (pcs_pds2d_run_persistent), one grid
-// barrier per iteration in place of the kernel boundary; iteration i reads (x0, z0) when i is
-// even and (x1, z1) when odd, as pcs_pds2d_run.  Needs hist (in-kernel loop control): after
-// each barrier every workgroup reads the same stop flag and the grid leaves together.
-template <int FK, int HK>
-__global__ __launch_bounds__(256) void k_pds2d_pt_loop(float* x0, float* x1, float* z0, float* z1,
-                                                        const float* __restrict__ gsrc, Slab32 s, Params<float> P,
-                                                        int gk, double* __restrict__ partials, Ctrl* ctrl,
-                                                        double* hist, void* ws, unsigned* bar, int niter, int tiles_x,
-                                                        Bands bd, int ntasks) {
-  __shared__ __attribute__((aligned(16))) float sm[PtGeom::SZ];
-  __shared__ double red[4 * 4];
-  __shared__ int flag[2];
-  int task;
-  {
-    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
-    task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
-  }
-  const int seg = task / tiles_x, strip = task - seg * tiles_x;
-  int s0, s1;
-  band_rows(bd, seg, s0, s1);
-  for (int i = 0; i < niter; ++i) {
-    if (threadIdx.x == 0) flag[0] = __hip_atomic_load(&ctrl->stopped, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (flag[0] != 0) break;  // uniform: written before the last barrier (solver.py:65-66)
-    const bool odd = i & 1;
-    double part[4] = {0.0, 0.0, 0.0, 0.0};
-    // sc1 stores: x'/z' leave the XCD's L2 as they are written, so the barrier's release
-    // has (almost) nothing dirty to write back
-    pt_task<FK, HK, 16>(odd ? x1 : x0, odd ? x0 : x1, odd ? z1 : z0, odd ? z0 : z1, gsrc, s, P, gk, s0, s1,
-                    strip * PtGeom::TW, sm, part);
-    block_sum<4>(part, red);
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag);
-    if (!grid_sync(bar, (unsigned)ntasks, flag)) break;
-  }
-}
-
 }  // namespace pcs

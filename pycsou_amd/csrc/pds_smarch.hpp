@@ -50,12 +50,6 @@ namespace pcs {
 #define PCS_SM_SAUX64 0
 #endif
 
-// step 0's z rows loaded and landed with the prologue's (1) or at step 0's top (0).  Parity green both
-// ways; no measurable difference on the 2048^2 legs (profiles/r3_ck44_ze_ab.txt): kept at 0
-#ifndef PCS_SM_ZEARLY
-#define PCS_SM_ZEARLY 0
-#endif
-
 // waves per SIMD the register budget targets (diagnostics builds override; 1 = no constraint)
 #ifndef PCS_SM_WPE
 #define PCS_SM_WPE 1
@@ -92,9 +86,10 @@ struct SParamsT {
 };
 using SParams = SParamsT<float>;
 
-// RS: 16-row halves per step (1: 16-row steps, 32-row rings; 2: 32-row steps, 64-row rings -- twice the
-// loads in flight per barrier, half the steps; fp32 only)
-template <int KK, int RS = 1>
+// 16-row steps, 32-row rings (32-row steps with 64-row rings measured no faster at 2048^2 and slower at
+// 4096^2, profiles/r4_sm_rs_ab.txt; z rows landed with the segment prologue's, profiles/r3_ck44_ze_ab.txt:
+// no change -- both removed in round 5)
+template <int KK>
 struct SMarch {
   static constexpr int TW = 64, TS = 16, D = KK == SK_LAP ? 1 : 2;
   // z rows [a + ZLO, a + ZHI] feed step a (U rows a+1..a+16 reach ZR rows up, ZD down; the Z
@@ -115,7 +110,7 @@ struct SMarch {
   // K u reaches left / right along axis 1 (the neighbour groups the Z phase reads; the U phase
   // reads both, its fifth column lying on either side)
   static constexpr bool Z_L = KK != PCS_FORWARD, Z_R = KK != PCS_BACKWARD;  // u[c-1] / u[c+1]
-  static constexpr int RING = 32 * RS, WZ = TW + 12, GZ = 18;  // ring rows of columns [c0 - 4, c0 + 68) (+ pad: 19 slots)
+  static constexpr int RING = 32, WZ = TW + 12, GZ = 18;  // ring rows of columns [c0 - 4, c0 + 68) (+ pad: 19 slots)
   static constexpr int RM = RING - 1;
   static constexpr int NZN = TS * GZ;                     // z items per component per step
   static constexpr int O_Z = 0, O_U = D * RING * WZ, SZ = O_U + RING * WZ;
@@ -123,7 +118,7 @@ struct SMarch {
 
 // T = float or double: the same geometry (4-column groups, 64-column strips, 16-row steps); an fp64
 // group is two 16-B accesses and the rings take twice the LDS (58 KB for a Gradient K)
-template <typename T, int KK, int FK, int HK, bool CI, int RS>
+template <typename T, int KK, int FK, int HK, bool CI>
 __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restrict__ xn,
                                             const T* __restrict__ z, T* __restrict__ zn,
                                             const T* __restrict__ gsrc, const T* __restrict__ bsrc,
@@ -133,9 +128,8 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
                                             double (&part)[4], int stop_raw) {
   constexpr uint32_t ES = sizeof(T);
   constexpr int SAUX = sizeof(T) == 4 ? PCS_SM_SAUX : PCS_SM_SAUX64;
-  using M = SMarch<KK, RS>;
+  using M = SMarch<KK>;
   constexpr int NT = 256, TS = M::TS, TW = M::TW, WZ = M::WZ, GZ = M::GZ, D = M::D, RING = M::RING, RM = M::RM;
-  static_assert(RS == 1 || (RS == 2 && !PCS_SM_ZEARLY), "32-row steps: z rows land at each step's top");
   constexpr int KZ = cdiv(M::NZN, NT);
   T* ZR = sm + M::O_Z;  // component d, row r: ZR + d * RING * WZ + (r & RM) * WZ; column c at c - c0 + 4
   T* UR = sm + M::O_U;
@@ -187,17 +181,14 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
     co_z[k] = col_off(c0 - 4 + 4 * g, n1, ES);
   }
   // x, y|g (and b) of the U items in two register sets: the set of step k + 1 loads at the top of
-  // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index; each
-  // set holds RS halves, index PB * RS + half)
-  G4<T> zr[RS][D][KZ], xr[2 * RS], gr[2 * RS], br[2 * RS], mr[2 * RS];
-#if PCS_SM_ZEARLY
-  G4<T> zr0[RS][D][KZ];  // step 0's z rows, loaded with the prologue's (landed before the prologue's U)
-#endif
-  T xe[2 * RS], ge[2 * RS], be[2 * RS], me[2 * RS];
+  // step k, a whole step before the U phase that reads it (PB: the set, a compile-time index)
+  G4<T> zr[D][KZ], xr[2], gr[2], br[2], mr[2];
+  T xe[2], ge[2], be[2], me[2];
 #pragma unroll
-  for (int i = 0; i < 2 * RS; ++i) xe[i] = ge[i] = be[i] = me[i] = T(0);
+  for (int i = 0; i < 2; ++i) xe[i] = ge[i] = be[i] = me[i] = T(0);
   // z rows [a + ZHI - 15, a + ZHI] (rows below rmin read as 0)
-  auto loads_z_into = [&](G4<T>(&dst)[D][KZ], int a, int rmin) {  // one 16-row half (step row a)
+  auto loads_z = [&](int a, int rmin) {
+    auto& dst = zr;
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
@@ -206,7 +197,8 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
         dst[d][k] = bload4t<T>(vz[d].r, (r < rmin ? kOOB : vz[d].row_off(r)) + co_z[k]);
       }
   };
-  auto land_z_from = [&](const G4<T>(&src)[D][KZ], int a) {
+  auto land_z = [&](int a) {
+    const auto& src = zr;
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
@@ -214,17 +206,8 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
         if (PCS_WAVE_ON(k, M::NZN))
           st4(ZR + d * RING * WZ + ((a + M::ZHI - 15 + rr_z[k]) & RM) * WZ + lo_z[k], src[d][k]);
   };
-  // a whole step: halves a, a + 16, ...
-  auto loads_z = [&](int a, int rmin) {
-#pragma unroll
-    for (int h = 0; h < RS; ++h) loads_z_into(zr[h], a + h * TS, rmin);
-  };
-  auto land_z = [&](int a) {
-#pragma unroll
-    for (int h = 0; h < RS; ++h) land_z_from(zr[h], a + h * TS);
-  };
-  // x and y|g of U row a + 1 + ui: the group and the fifth column (PB: slot set * RS + half)
-  auto loads_x1 = [&](auto pb, int a, int rmin) {
+  // x and y|g of U row a + 1 + ui: the group and the fifth column (PB: the register set)
+  auto loads_x = [&](auto pb, int a, int rmin) {
     constexpr int PB = decltype(pb)::value;
     const int r = a + 1 + ui;
     const uint32_t ro = r < rmin ? kOOB : vx.row_off(r);
@@ -246,11 +229,6 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
       br[PB] = bload4t<T>(vb.r, rb + co_c);
       be[PB] = bload1t<T>(vb.r, rb + co_e);
     }
-  };
-  auto loads_x = [&](auto pb, int a, int rmin) {  // every half of set PB
-    constexpr int PB = decltype(pb)::value;
-    loads_x1(std::integral_constant<int, PB * RS>{}, a, rmin);
-    if constexpr (RS == 2) loads_x1(std::integral_constant<int, PB * RS + 1>{}, a + TS, rmin);
   };
 
   // ---- U: x_t, u on row lr = a + 1 + ui, columns c .. c + 3 and ce; x' on own cells
@@ -420,68 +398,40 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
   // rows it does not need, register set 0 half 0), x' on row s0
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
-  const int nsteps = (s1 - s0 + TS * RS - 1) / (TS * RS);
-#if PCS_SM_ZEARLY
-  // step 0's z rows [s0 + ZHI - 15, s0 + ZHI] and the prologue's [s0 + ZHI - 31, s0 + ZHI - 16] fill the
-  // 32-row ring exactly: both load here and land before the prologue's U (one exposed load latency
-  // instead of two); the prologue's own U rows read no row of step 0's set
-  static_assert(M::ZHI - 15 > (KK == SK_LAP ? 2 : KK == PCS_FORWARD ? 0 : 1),
-                "the prologue's own U rows (<= s0) read no z row of step 0's set");
-  if (nsteps > 0) loads_z_into(zr0[0], s0, -(1 << 30));
-  loads_z_into(zr[0], s0 - TS, s0 - M::ZPRO);
-  loads_x1(P0{}, s0 - TS, s0 - M::UPRO);
-  if (nsteps > 0) loads_x(P1{}, s0, -(1 << 30));
+  const int nsteps = (s1 - s0 + TS - 1) / TS;
+  loads_z(s0 - TS, s0 - M::ZPRO);
+  loads_x(P0{}, s0 - TS, s0 - M::UPRO);
   lds_barrier();  // rings zeroed
-  land_z_from(zr[0], s0 - TS);
-  if (nsteps > 0) land_z_from(zr0[0], s0);
-#else
-  loads_z_into(zr[0], s0 - TS, s0 - M::ZPRO);
-  loads_x1(P0{}, s0 - TS, s0 - M::UPRO);
-  lds_barrier();  // rings zeroed
-  land_z_from(zr[0], s0 - TS);
+  land_z(s0 - TS);
   if (nsteps > 0) {
     loads_z(s0, -(1 << 30));
     loads_x(P1{}, s0, -(1 << 30));
   }
-#endif
   if (stop_raw) return;  // loop already stopped (solver.py:65-66): loads issued, nothing stored
   lds_barrier();
   uphase(std::false_type{}, P0{}, s0 - TS);
   // step k reads register set PB = (k + 1) & 1 and loads the other one for step k + 1
-  using H1 = std::integral_constant<int, RS - 1>;  // the second half's offset in a set (RS = 2)
   auto step = [&](auto pb, int k) {
     constexpr int PB = decltype(pb)::value;
-    using U0 = std::integral_constant<int, PB * RS>;
-    using U1 = std::integral_constant<int, PB * RS + H1::value>;
-    const int a = s0 + k * TS * RS;
-    // rows [a, a + 16 RS] at >= 2 rows from both image edges (uniform)
-    const bool ri = s.row0 + a >= 2 && s.row0 + a + TS * RS + 3 <= n0;
+    const int a = s0 + k * TS;
+    // rows [a, a + 16] at >= 2 rows from both image edges (uniform)
+    const bool ri = s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0;
     lds_barrier();  // the previous step's Z phase is done with the rings
-    if (!PCS_SM_ZEARLY || k > 0) land_z(a);
+    land_z(a);
     if (PCS_SM_PRIO) __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
     if (k + 1 < nsteps) {
-      loads_z(a + TS * RS, -(1 << 30));
-      loads_x(std::integral_constant<int, 1 - PB>{}, a + TS * RS, -(1 << 30));
+      loads_z(a + TS, -(1 << 30));
+      loads_x(std::integral_constant<int, 1 - PB>{}, a + TS, -(1 << 30));
     }
     if (PCS_SM_PRIO) __builtin_amdgcn_s_setprio(0);
     lds_barrier();
-    // U reads only the z ring; the Z rows of a half read u rows up to its last row + 1 (+ 2 on the
-    // image's first row only), all written by this step's U halves or earlier
-    if (ri) {
-      uphase(std::true_type{}, U0{}, a);
-      if constexpr (RS == 2) uphase(std::true_type{}, U1{}, a + TS);
-    } else {
-      uphase(std::false_type{}, U0{}, a);
-      if constexpr (RS == 2) uphase(std::false_type{}, U1{}, a + TS);
-    }
+    // U reads only the z ring; the Z rows read u rows up to their last row + 1 (+ 2 on the image's
+    // first row only), all written by this step's U phase or earlier
+    if (ri) uphase(std::true_type{}, pb, a);
+    else uphase(std::false_type{}, pb, a);
     lds_barrier();
-    if (ri) {
-      zphase(std::true_type{}, a);
-      if constexpr (RS == 2) zphase(std::true_type{}, a + TS);
-    } else {
-      zphase(std::false_type{}, a);
-      if constexpr (RS == 2) zphase(std::false_type{}, a + TS);
-    }
+    if (ri) zphase(std::true_type{}, a);
+    else zphase(std::false_type{}, a);
   };
   for (int k = 0; k < nsteps; k += 2) {
     step(P1{}, k);
@@ -491,7 +441,7 @@ __device__ __forceinline__ void smarch_task(const T* __restrict__ x, T* __restri
 #undef PCS_ITEM
 }
 
-template <typename T, int KK, int FK, int HK, int RS = 1>
+template <typename T, int KK, int FK, int HK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE))) void k_pds2d_smarch(const T* __restrict__ x, T* __restrict__ xn,
                                                        const T* __restrict__ z, T* __restrict__ zn,
                                                        const T* __restrict__ gsrc,
@@ -500,7 +450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
                                                        SParamsT<T> Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
                                                        double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
                                                        int ntasks) {
-  __shared__ __attribute__((aligned(16))) T sm[SMarch<KK, RS>::SZ];
+  __shared__ __attribute__((aligned(16))) T sm[SMarch<KK>::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
   const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
@@ -518,10 +468,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
     if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
-      smarch_task<T, KK, FK, HK, true, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
+      smarch_task<T, KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
                                            stop_raw);
     else
-      smarch_task<T, KK, FK, HK, false, RS>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
+      smarch_task<T, KK, FK, HK, false>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
                                             stop_raw);
   }
   if (stop_raw) return;  // the task returned before any store

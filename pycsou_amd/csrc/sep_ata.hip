@@ -324,113 +324,24 @@ static int ata_padb(int kb, int offb) {
 // Two barriers per step; the next step's input rows are in flight (registers) during PH and PV.
 // The tables (a for both axes, the four 7x7 edge blocks) are built per workgroup from the taps
 // in fp64.  2 words of HBM traffic per voxel, like one k_sep2d_march pass, for the work of two.
-// diagnostic ablation builds only (-DPCS_NRM_ABL=bits, tools/build_var.sh): 1 = output stores
-// dropped, 2 / 4 = PH / PV reduced to their centre tap, 8 = input loads read nothing
-#ifndef PCS_NRM_ABL
-#define PCS_NRM_ABL 0
-#endif
-#ifndef PCS_NRM_PHU  // PH items unrolled per loop trip; diagnostics
-#define PCS_NRM_PHU 1
-#endif
-#ifndef PCS_NRM_PRIO  // wave priority 3 while the next step's loads issue; diagnostics
-#define PCS_NRM_PRIO 0
-#endif
-#ifndef PCS_NRM_CH  // PV window rows per pipelined chunk (0: 4); diagnostics
-#define PCS_NRM_CH 0
-#endif
-#ifndef PCS_NRM_PF2  // staged rows loaded two steps ahead (two register sets); diagnostics
-#define PCS_NRM_PF2 0
-#endif
-#ifndef PCS_NRM_PK  // fp32 PV taps as v_pk_fma_f32 on column pairs (tap broadcast); diagnostics
-#define PCS_NRM_PK 0
-#endif
-// lane-rotated 16-B chunk order of the LDS writes (below): parity green, no measurable change (512^3 fp32
-// 0.463-0.478 against 0.454-0.487 ms, 1024^3 fp64 5.46-5.48 against 5.49, C4 631 it/s both ways,
-// profiles/r4_nrm_swz_ab.txt) -- off; diagnostics builds set 1
-#ifndef PCS_NRM_SWZ
-#define PCS_NRM_SWZ 0
-#endif
-
-// NC consecutive 16-B chunks v (chunk j at p + j 16 B) written in the lane's order k -> chunk k ^ xm: the 8
-// lanes of a ds_write_b128 group (banks (a / 4) mod 32) whose items lie NC chunks apart then hit 8 distinct
-// 16-B slots when xm spreads them (xm from the lane's item index; 0 = plain order)
-template <typename T, int NC>
-__device__ __forceinline__ void nrm_st_chunks(T* p, const T* v, int xm) {
-  constexpr int VN = 16 / (int)sizeof(T);
-  T w[NC * VN];
-#pragma unroll
-  for (int i = 0; i < NC * VN; ++i) w[i] = v[i];
-  if (PCS_NRM_SWZ) {  // butterfly: w chunk k <- v chunk k ^ xm
-#pragma unroll
-    for (int b = 1; b < NC; b <<= 1) {
-      const bool sw = (xm & b) != 0;
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-        if (!(j & b))
-#pragma unroll
-          for (int e = 0; e < VN; ++e) {
-            const T a = w[j * VN + e], c = w[(j | b) * VN + e];
-            w[j * VN + e] = sw ? c : a;
-            w[(j | b) * VN + e] = sw ? a : c;
-          }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NC; ++k) {
-    V16<T> c;
-#pragma unroll
-    for (int e = 0; e < VN; ++e) c.v[e] = w[k * VN + e];
-    stv(p + VN * (PCS_NRM_SWZ ? (k ^ xm) : k), c);
-  }
-}
-template <typename T, int TX_, int RS_, int RB_, int PQ_>
-struct NrmG {
-  static constexpr int PQ = PQ_;  // PH item: 4 PQ outputs of one row
-  static constexpr int TX = TX_, RS = RS_, RB = RB_, RING = RS + 28, GX = TX / 4, GI = GX + 8;
-  // fp64 LDS bank layout: a 4-column group is 32 B, so the 16 lanes of a ds_read_b128 group span 512 B;
-  // the staged rows get an odd 16-B slot pitch (PH reads rows r, r + 1 in one lane group) and the ring
-  // rows a pitch of TX + PAD with row pairs alternating a 16-B offset inside it (PV reads rows r, r + 2:
-  // 2 (TX + PAD) +- PAD elements apart = an odd number of 16-B slots mod 256 B): every b128 lane group
-  // then hits 16 distinct slots (fp64 PMC before: 16.3 M bank-conflict cycles per launch at 4096^2,
-  // profiles/r4_prof_c3f64_*).  A row never reaches the next one's first element.
-  // fp32 with 8- / 16-output PH items: the lanes of a group read every other (every fourth) 16-B slot of
-  // rows r, r + 1 (.. r + 3), so the staged rows take an odd slot pitch too (4 floats; 22.4 M bank-conflict
-  // cycles per 512^3 launch without it at 8 outputs, profiles/r4_prof_nrm32_pmc_summary.txt)
-  static constexpr int PAD = sizeof(T) == 8 ? 2 : 0, SPAD = sizeof(T) == 8 ? 2 : PQ >= 2 ? 4 : 0;
-  static constexpr int WI = 4 * GI + SPAD, TP = TX + PAD;
-  static __device__ __forceinline__ int rrow(int slot) { return slot * TP + ((slot >> 1) & 1) * PAD; }
+// fp32 geometry (fp64 takes k_sep2d_nrmm below): 128-column strips, 32-row steps, PV items of 4 rows x
+// 4 columns, PH items of 16 outputs (0.433-0.449 against 0.469 ms for 8 at 512^3, C4 642-645 against
+// 633-635 it/s, profiles/r4_nrm_cfg6_ab.txt).  Measured without gain and removed in round 5: loads two
+// steps ahead, packed-FMA PV, PH unroll, PV chunks of 2 / 8 rows, lane-rotated LDS writes
+// (profiles/r4_nrm_var_ab*.txt, r4_nrm_swz_ab.txt)
+struct NrmF {
+  static constexpr int PQ = 4;  // PH item: 4 PQ outputs of one row
+  static constexpr int TX = 128, RS = 32, RB = 4, RING = RS + 28, GX = TX / 4, GI = GX + 8;
+  // the lanes of a b128 group read every fourth 16-B slot of rows r .. r + 3, so the staged rows take an
+  // odd slot pitch (22.4 M bank-conflict cycles per 512^3 launch without it at 8 outputs,
+  // profiles/r4_prof_nrm32_pmc_summary.txt)
+  static constexpr int SPAD = 4, WI = 4 * GI + SPAD, TP = TX;
   static constexpr int NT = (RS / RB) * GX, NIN = RS * GI, NL = (NIN + NT - 1) / NT, NPH = RS * GX / PQ;
-  static constexpr int NST = RB * (int)sizeof(T) / 4;  // 16-B stores per thread per step
+  static constexpr int NST = RB;  // 16-B stores per thread per step
   static constexpr int NTAB = 288;  // a_v[0..29), a_h[32..61), E_v lo / hi, E_h lo / hi (7 x 8 each)
   static_assert(NPH % NT == 0, "whole PH items per thread");
-  static constexpr size_t lds_bytes() { return sizeof(T) * ((size_t)RS * WI + (size_t)RING * TP + NTAB); }
+  static constexpr size_t lds_bytes() { return 4 * ((size_t)RS * WI + (size_t)RING * TP + NTAB); }
 };
-template <typename T> struct NrmCfg;
-// wider PH items since round 4 -- 8 outputs (PQ 2): 512^3 fp32 0.483 against 0.495-0.500 ms, 1024^3 fp64
-// 5.32-5.34 against 5.52-5.57 ms, 4096^2 fp64 0.105-0.107 against 0.108-0.109 ms (profiles/r4_nrm_var_ab.txt);
-// fp32 16 outputs (PQ 4): 0.433-0.449 against 0.469 ms, C4 642-645 against 633-635 it/s
-// (profiles/r4_nrm_cfg6_ab.txt).  PCS_NRM_CFG=0 (diagnostics): the 4-output items
-#ifndef PCS_NRM_CFG
-#define PCS_NRM_CFG 2
-#endif
-#if PCS_NRM_CFG == 0
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 1>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 1>; };
-#elif PCS_NRM_CFG == 2  // 256 threads, 16-output (fp32) / 8-output (fp64) PH items
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 4>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
-#elif PCS_NRM_CFG == 6  // diagnostics: fp32 8-output PH items
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 2, 2>; };
-#elif PCS_NRM_CFG == 5  // diagnostics: fp64 16-row steps, 128 threads (36 KB of LDS: 4 workgroups / CU)
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 4, 2>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 16, 2, 2>; };
-#else  // diagnostics: 128 threads, RB 8 / 4 and 16 / 8-output PH items -- fewer LDS bytes per
-       // output (38 against 77 B in fp32) but half the waves: 0.69 against 0.57 ms (512^3 fp32),
-       // 9.4 against 7.8 ms (1024^3 fp64), profiles/r2_nrm_ablation.txt
-template <> struct NrmCfg<float> { using G = NrmG<float, 128, 32, 8, 4>; };
-template <> struct NrmCfg<double> { using G = NrmG<double, 64, 32, 4, 2>; };
-#endif
 
 // compiler fences of the PV chunks: no LDS read or FMA moves across (bounds the registers held
 // by hoisted window reads) ...
@@ -457,24 +368,11 @@ __device__ __forceinline__ void nrm_bstore(Rsrc r, uint32_t off, const Q4<T>& a)
   }
 }
 
-// a += h w on 4 columns: two packed FMAs in fp32 (PCS_NRM_PK), four scalar ones otherwise
+// a += h w on 4 columns
 template <typename T>
 __device__ __forceinline__ void nrm_fma4(Q4<T>& a, T h, const Q4<T>& w) {
-  if constexpr (sizeof(T) == 4 && PCS_NRM_PK) {
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    const f2v hh = {h, h};
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      f2v ap = {a.v[2 * p], a.v[2 * p + 1]};
-      const f2v wp = {w.v[2 * p], w.v[2 * p + 1]};
-      ap = __builtin_elementwise_fma(hh, wp, ap);
-      a.v[2 * p] = ap.x;
-      a.v[2 * p + 1] = ap.y;
-    }
-  } else {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) a.v[m] += h * w.v[m];
-  }
+  for (int m = 0; m < 4; ++m) a.v[m] += h * w.v[m];
 }
 
 // tap d of a filter stored as h[0..k) with offset off (zero outside)
@@ -496,21 +394,23 @@ __device__ __forceinline__ Q4<T> nrm_bload(Rsrc r, uint32_t off) {
   return a;
 }
 
-// SUB: out = C^T C in - sub (sub laid out as in / out; the fp64 2-D step's grad F = N x - Conv^T y formed
-// here, so the step reads one buffer instead of two -- the same subtraction, bit for bit)
+// SUB: out = C^T C in - sub (sub laid out as in / out; a 2-D step's grad F = N x - Conv^T y formed here, so
+// the step reads one buffer instead of two -- the same subtraction, bit for bit).  fp32 (T = float): 53 KB of
+// LDS, 3 workgroups / CU
 template <typename T, bool SUB>
-__global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
+__global__ __launch_bounds__(NrmF::NT, 3) void k_sep2d_nrm(const T* __restrict__ in, T* __restrict__ out, int n1,
                                                                  int n2, int nstrips, int nseg, int seg_len,
                                                                  int64_t ntasks, const T* __restrict__ ha_, int ka,
                                                                  int offa, const T* __restrict__ hb_, int kb, int offb,
                                                                  const T* __restrict__ sub) {
-  using G = typename NrmCfg<T>::G;
+  static_assert(sizeof(T) == 4, "fp32 (fp64: k_sep2d_nrmm)");
+  using G = NrmF;
   constexpr int TX = G::TX, RS = G::RS, RB = G::RB, RING = G::RING, GX = G::GX, GI = G::GI, WI = G::WI, NT = G::NT,
-                NL = G::NL;
+                NL = G::NL, TP = G::TP;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* stg = reinterpret_cast<T*>(smem_raw);  // RS x WI staged input rows
-  T* ring = stg + RS * WI;                  // RING rows (pitch TP, G::rrow) of the horizontal pass
-  T* tab = ring + RING * G::TP;             // NTAB
+  T* ring = stg + RS * WI;                  // RING rows (pitch TP) of the horizontal pass
+  T* tab = ring + RING * TP;                // NTAB
   const int tid = threadIdx.x;
   {
     __shared__ double hs[32];  // the two filters in fp64
@@ -589,7 +489,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       const int e = min(l * NT + tid, G::NIN - 1);
       const int rr = e / GI, gg = e - rr * GI;
       const int k = c.s * RS + rr, gi = c.a - 14 + k, gc = gc0 + 4 * gg;
-      const bool ok = gi >= 0 && gi < n1 && k <= kmax && gc >= 0 && gc + 4 <= n2 && !(PCS_NRM_ABL & 8);
+      const bool ok = gi >= 0 && gi < n1 && k <= kmax && gc >= 0 && gc + 4 <= n2;
       const Q4<T> v = ldq(src + (ok ? (int64_t)gi * n2 + gc : 0));
 #pragma unroll
       for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
@@ -603,18 +503,8 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       const int e = l * NT + tid, rr = e / GI, gg = e - rr * GI;
-      // fp64: a group is 2 chunks, 8 lanes span 256 B: the second 4 lanes write their second chunk first
-      if (e < G::NIN) nrm_st_chunks<T, 4 / V16<T>::N>(stg + rr * WI + 4 * gg, q[l].v, (gg >> 2) & (4 / V16<T>::N - 1));
+      if (e < G::NIN) stq(stg + rr * WI + 4 * gg, q[l]);
     }
-  };
-  auto issue = [&](const Cur& c, Q4<T>(&q)[NL]) {
-#if PCS_NRM_PRIO
-    __builtin_amdgcn_s_setprio(3);
-#endif
-    prefetch(c, q);
-#if PCS_NRM_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
   };
   // one step on the staged rows of cur: PH into the ring, PV from it -> HBM
   auto body = [&](const Cur cur) {
@@ -635,7 +525,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
     lds_barrier();
     // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q);
     // an item is 4 PQ consecutive outputs of one row (PQ + 8 window reads)
-#pragma unroll PCS_NRM_PHU
+#pragma unroll 1
     for (int l = 0; l < G::NPH / NT; ++l) {
       constexpr int PQ = G::PQ, GQ = GX / PQ;
       const int e = l * NT + tid, r = e / GQ, g = PQ * (e - r * GQ);
@@ -651,8 +541,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #pragma unroll
           for (int o = 0; o < 4 * PQ; ++o) {
             const int qq = 4 * u + ee - o - 2;
-            if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 2) || qq == 14))
-              acc[o] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
+            if (qq >= 0 && qq < 29) acc[o] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
           }
       }
       const int col = c0 + 4 * g;
@@ -670,10 +559,12 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
       }
       int slot = sb + r;
       slot = slot >= RING ? slot - RING : slot;
-      {  // NC chunks per item, items NC chunks apart: rotate by the item index's bits above 8 / NC lanes
-        constexpr int NC = 4 * PQ / V16<T>::N, LNC = NC >= 4 ? 2 : NC == 2 ? 1 : 0;
-        const int gi = e - r * GQ;
-        nrm_st_chunks<T, NC>(ring + G::rrow(slot) + 4 * g, acc, (gi >> (3 - LNC)) & (NC - 1));
+#pragma unroll
+      for (int k = 0; k < PQ; ++k) {
+        Q4<T> c;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) c.v[m] = acc[4 * k + m];
+        stq(ring + slot * TP + 4 * (g + k), c);
       }
     }
     lds_barrier();
@@ -688,7 +579,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
         for (int m = 0; m < 4; ++m) acc[rr].v[m] = T(0);
       // RB + 28 window rows in chunks of CH, the next chunk's reads in flight during this one's FMAs
       // 4-row chunks: 0.543 against 0.565-0.573 ms for 8 (512^3 fp32, profiles/r2_nrm_ablation.txt)
-      constexpr int NV = RB + 28, CH = PCS_NRM_CH > 0 ? PCS_NRM_CH : 4, NCH = (NV + CH - 1) / CH;
+      constexpr int NV = RB + 28, CH = 4, NCH = (NV + CH - 1) / CH;
       const T* rcol = ring + 4 * vg;
       Q4<T> w[2][CH];  // chunk c in w[c & 1] (static after unrolling: no register copies)
       auto rd = [&](int c, Q4<T>(&wc)[CH]) {
@@ -697,7 +588,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
           if (c * CH + j < NV) {
             int slot = base + c * CH + j;
             slot = slot >= RING ? slot - RING : slot;
-            wc[j] = ldsq(rcol + G::rrow(slot));
+            wc[j] = ldsq(rcol + slot * TP);
           }
         }
       };
@@ -713,9 +604,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #pragma unroll
             for (int rr = 0; rr < RB; ++rr) {
               const int qq = v - rr;
-              if (qq >= 0 && qq < 29 && (!(PCS_NRM_ABL & 4) || qq == 14)) {
-                nrm_fma4(acc[rr], av[qq < 14 ? 14 - qq : qq - 14], w[c & 1][j]);
-              }
+              if (qq >= 0 && qq < 29) nrm_fma4(acc[rr], av[qq < 14 ? 14 - qq : qq - 14], w[c & 1][j]);
             }
           }
         }
@@ -737,7 +626,7 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
             const int jr = top ? i : i - (n1 - 7), row0 = top ? 0 : n1 - 7;
             const T* e = top ? evl : evh;
             for (int c = 0; c < 7; ++c) {
-              const Q4<T> w = ldsq(ring + G::rrow((row0 + c - cur.a + 14) % RING) + 4 * vg);
+              const Q4<T> w = ldsq(ring + ((row0 + c - cur.a + 14) % RING) * TP + 4 * vg);
               const T ec = e[8 * jr + c];
 #pragma unroll
               for (int m = 0; m < 4; ++m) acc[rr].v[m] -= ec * w.v[m];
@@ -748,13 +637,338 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
 #pragma unroll
           for (int m = 0; m < 4; ++m) acc[rr].v[m] = acc[rr].v[m] - bsub[rr].v[m];
         }
-        nrm_bstore(dst, live && !(PCS_NRM_ABL & 1) ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB, acc[rr]);
+        nrm_bstore(dst, live ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB, acc[rr]);
       }
     }
   };
-#if PCS_NRM_PF2
-  // the step after c (more = false: none; c itself is returned)
-  auto advance = [&](const Cur& c, bool& more) {
+  Q4<T> q[NL];
+  Cur cur = task_at(t0);
+  prefetch(cur, q);
+  for (;;) {
+    // the previous step's RB row stores may still be in flight
+    stage(q, std::integral_constant<int, G::NST>{});
+    Cur nxt = cur;
+    bool more = true;
+    if (cur.s + 1 < cur.ns) {
+      nxt.s = cur.s + 1;
+    } else {
+      more = cur.t + t_stride < t_end;
+      if (more) nxt = task_at(cur.t + t_stride);
+    }
+    prefetch(nxt, q);  // unconditional (the last step re-reads its own rows): the wait for these
+                    // loads at the next step then leaves this step's stores in flight
+    body(cur);
+    if (!more) break;
+    cur = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_sep2d_nrmm: the same two 29-tap passes on a MIRRORED ring (round 5).  The vertical window of a PV
+// item spans RB + 28 ring rows; with the ring's first RB + 27 rows duplicated past its end (PH writes
+// those rows twice) every window is contiguous, so its reads are one base address plus immediate
+// offsets -- the old kernel recomputed a wrapped slot and its row offset for each of the 30 window rows
+// (about 7 VALU per row pair, 227 VALU beside 232 FMAs in the fp64 PV block).  PV items are RB = 4 rows x
+// one 16-B chunk (4 floats / 2 doubles): RB + 28 = 32 b128 reads per 4 x VN outputs (fp64: 4 reads per
+// output instead of 7.5).  LDS layouts, all conflict-free in the lane-group model of MI355X_MICROARCH.md
+// (ds_read_b128: 16-lane groups, 64 banks; ds_write_b128: 8-lane groups, 32 banks):
+//   staged rows  pitch WI = the row's 4-column groups + 4 16-B slots, row r shifted by (r & 3) slots;
+//                staging items in row-major order (fp32) / 8-lane groups of 4 groups x 2 rows (fp64)
+//   PH items     lane l of wave w: row 8 w + (l & 7), item (l >> 3) & 7 of the row's 8 (4 PQ outputs, 4
+//                chunks each): the 8 lanes of a write group hold 8 rows of one item column
+//   ring         pitch TP = TX + one 16-B slot (an odd number of slots: those 8 rows hit 8 banks)
+//   PV items     the 32 lanes of a half-wave read 32 consecutive chunks of one ring row
+// one 16-B chunk from LDS as a single ds_read_b128 (volatile LDS access, as ldsq)
+template <typename T>
+__device__ __forceinline__ V16<T> nrm_ldsv(const T* p) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const volatile u4* lds_u4;
+  V16<T> r;
+  const u4 v = *((lds_u4)(p));
+  __builtin_memcpy(r.v, &v, 16);
+  return r;
+}
+
+template <typename T>
+struct NrmM {
+  static constexpr int ES = sizeof(T), VN = 16 / ES;
+  static constexpr int TX = ES == 4 ? 128 : 64, PQ = ES == 4 ? 4 : 2;  // 8 PH items of 4 chunks per row
+  static constexpr int RS = 32, RB = 4, RING = RS + 28, MIR = RB + 27;
+  static constexpr int GX = TX / 4, GI = GX + 8, GQ = GX / PQ, GV = TX / VN;
+  static constexpr int NT = (RS / RB) * GV;
+  static constexpr int WI = 4 * GI + 4 * VN;  // staged pitch (elements): the groups + 4 slots of shift room
+  static constexpr int TP = TX + VN;          // ring pitch
+  static constexpr int NIN = RS * GI, NL = (NIN + NT - 1) / NT;
+  static constexpr int NTAB = 288;
+  static_assert(GQ == 8 && NT == 256 && RS * GQ == NT && GI % 4 == 0, "one PH item per thread");
+  static constexpr size_t lds_bytes() { return ES * ((size_t)RS * WI + (size_t)(RING + MIR) * TP + NTAB); }
+  // staging item e -> staged row / 4-column group
+  static __device__ __forceinline__ void stage_item(int e, int& rr, int& gg) {
+    if constexpr (ES == 4) {
+      rr = e / GI;
+      gg = e - rr * GI;
+    } else {
+      const int e8 = e & 7, eh = e >> 3, q = eh / (GI / 4);
+      rr = 2 * q + (e8 >> 2);
+      gg = 4 * (eh - q * (GI / 4)) + (e8 & 3);
+    }
+  }
+  static __device__ __forceinline__ int srow(int r) { return r * WI + (r & 3) * VN; }
+};
+
+template <typename T, bool SUB>
+__global__ __launch_bounds__(256, 2) void k_sep2d_nrmm(const T* __restrict__ in, T* __restrict__ out, int n1, int n2,
+                                                       int nstrips, int nseg, int seg_len, int64_t ntasks,
+                                                       const T* __restrict__ ha_, int ka, int offa,
+                                                       const T* __restrict__ hb_, int kb, int offb,
+                                                       const T* __restrict__ sub) {
+  using G = NrmM<T>;
+  constexpr int TX = G::TX, RS = G::RS, RB = G::RB, RING = G::RING, GV = G::GV, VN = G::VN, NT = G::NT,
+                NL = G::NL, TP = G::TP, PQ = G::PQ;
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* stg = reinterpret_cast<T*>(smem_raw);  // RS staged input rows (pitch WI, shifted)
+  T* ring = stg + RS * G::WI;               // RING + MIR rows of the horizontal pass (pitch TP)
+  T* tab = ring + (RING + G::MIR) * TP;     // NTAB
+  const int tid = threadIdx.x;
+  {
+    __shared__ double hs[32];  // the two filters in fp64
+    if (tid < 16) hs[tid] = tid < ka ? (double)ha_[tid] : 0.0;
+    else if (tid < 32) hs[tid] = tid - 16 < kb ? (double)hb_[tid - 16] : 0.0;
+    __syncthreads();
+    for (int e = tid; e < G::NTAB; e += NT) {
+      double v = 0.0;
+      if (e < 64) {
+        const int q = e & 31;
+        const double* h = e < 32 ? hs : hs + 16;
+        const int k = e < 32 ? ka : kb, off = e < 32 ? offa : offb;
+        if (q < 29)
+          for (int m = -7; m <= 7; ++m) v += nrm_tap(h, k, off, m) * nrm_tap(h, k, off, m + q - 14);
+      } else {
+        const int idx = e - 64, tb = idx / 56, r = idx - 56 * tb, j = r >> 3, c = r & 7;
+        const double* h = tb < 2 ? hs : hs + 16;
+        const int k = tb < 2 ? ka : kb, off = tb < 2 ? offa : offb;
+        if (c < 7) {
+          if ((tb & 1) == 0)  // rows / columns i = -7..-1 before the plane: E[j][c], j, c < 7
+            for (int i = -7; i < 0; ++i) v += nrm_tap(h, k, off, i - j) * nrm_tap(h, k, off, i - c);
+          else  // after it: j = n - 7 + jj, c = n - 7 + cc, i = n + ii
+            for (int ii = 0; ii < 7; ++ii) v += nrm_tap(h, k, off, 7 + ii - j) * nrm_tap(h, k, off, 7 + ii - c);
+        }
+      }
+      tab[e] = (T)v;
+    }
+    __syncthreads();
+  }
+  // the autocorrelation is symmetric: window tap q is a[|q - 14|], 15 registers per axis
+  T av[15], ah[15];
+#pragma unroll
+  for (int e = 0; e < 15; ++e) {
+    av[e] = tab[14 + e];
+    ah[e] = tab[32 + 14 + e];
+  }
+  const T* evl = tab + 64;
+  const T* evh = tab + 120;
+  const T* ehl = tab + 176;
+  const T* ehh = tab + 232;
+  int64_t t0, t_end, t_stride;
+  {  // XCD x owns a contiguous share of the task list; its blocks take consecutive tasks
+    const int64_t b = blockIdx.x, nb = gridDim.x, xcd = b % 8, k = b / 8, q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (xcd < r ? 1 : 0);
+    const int64_t before = xcd * q + (xcd < r ? xcd : r);
+    const int64_t lo = ntasks * before / nb, hi = ntasks * (before + nbx) / nb;
+    t0 = lo + k;
+    t_end = hi;
+    t_stride = nbx;
+  }
+  if (t0 >= t_end) return;
+  struct Cur {
+    int64_t t, plane;
+    int strip, a, b, s, ns;
+  };
+  auto task_at = [&](int64_t t) {
+    Cur c;
+    c.t = t;
+    const int64_t per_plane = (int64_t)nseg * nstrips;
+    c.plane = t / per_plane;
+    const int rem = (int)(t - c.plane * per_plane), seg = rem / nstrips;
+    c.strip = rem - seg * nstrips;
+    c.a = seg * seg_len;
+    c.b = min(n1, c.a + seg_len);
+    c.s = 0;
+    c.ns = (c.b - c.a + 28 + RS - 1) / RS;
+    return c;
+  };
+  // this thread's staging items (fixed): staged row / group and their LDS offsets
+  int st_rr[NL], st_gg[NL], st_off[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    G::stage_item(min(l * NT + tid, G::NIN - 1), st_rr[l], st_gg[l]);
+    st_off[l] = G::srow(st_rr[l]) + 4 * st_gg[l];
+  }
+  // staged rows of step s: input rows a - 14 + s RS + rr, columns c0 - 16 + 4 gg (0 outside)
+  auto prefetch = [&](const Cur& c, Q4<T>(&q)[NL]) {
+    const T* src = in + c.plane * (int64_t)n1 * n2;
+    const int kmax = c.b - c.a + 27;  // last staged row any output of [a, b) reads
+    const int gc0 = c.strip * TX - 16;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int k = c.s * RS + st_rr[l], gi = c.a - 14 + k, gc = gc0 + 4 * st_gg[l];
+      const bool ok = gi >= 0 && gi < n1 && k <= kmax && gc >= 0 && gc + 4 <= n2;
+      const Q4<T> v = ldq(src + (ok ? (int64_t)gi * n2 + gc : 0));
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[l].v[m] = ok ? v.v[m] : T(0);
+    }
+  };
+  // the staged rows have landed (WN: the memory ops issued after them that may stay in flight --
+  // vector memory ops retire in order); rows -> LDS
+  auto stage = [&](const Q4<T>(&q)[NL], auto waitn) {
+    constexpr int WN = decltype(waitn)::value;
+    __builtin_amdgcn_s_waitcnt((WN & 15) | ((WN >> 4) << 14) | (7 << 4) | (15 << 8));
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+      if (l * NT + tid < G::NIN) stq(stg + st_off[l], q[l]);
+  };
+  // PH item: row pr, outputs 4 PQ pg .. + 4 PQ - 1 of the strip
+  const int pr = ((tid >> 6) << 3) | (tid & 7), pg = PQ * ((tid >> 3) & 7);
+  const T* psrow = stg + G::srow(pr);
+  // PV item: rows RB vi .. + RB - 1 of the step, chunk vg (columns VN vg .. VN vg + VN - 1)
+  const int vi = tid / GV, vg = tid - vi * GV, r0 = RB * vi;
+  auto body = [&](const Cur cur) {
+    const int c0 = cur.strip * TX;
+    const int gc = c0 + VN * vg;
+    V16<T> bsub[SUB ? RB : 1];  // SUB: the PV outputs' sub values, loaded before PH (a phase to land)
+    if constexpr (SUB) {
+      const Rsrc rs = rsrc_of(sub + cur.plane * (int64_t)n1 * n2, (uint32_t)((int64_t)n1 * n2 * sizeof(T)));
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr) {
+        const int i = cur.a - 28 + cur.s * RS + r0 + rr;
+        const bool live = i >= cur.a && i < cur.b && gc < n2;
+        const u4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(live ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB), 0, 0);
+        __builtin_memcpy(bsub[rr].v, &d, 16);
+      }
+    }
+    lds_barrier();
+    // ---- PH: t[row][c0 + j] = sum_q a_h[q] x[row][c0 + j - 14 + q] (staged column j + 2 + q)
+    {
+      T acc[4 * PQ];
+#pragma unroll
+      for (int o = 0; o < 4 * PQ; ++o) acc[o] = T(0);
+#pragma unroll
+      for (int u = 0; u < PQ + 8; ++u) {
+        const Q4<T> v = ldsq(psrow + 4 * (pg + u));
+#pragma unroll
+        for (int ee = 0; ee < 4; ++ee)
+#pragma unroll
+          for (int o = 0; o < 4 * PQ; ++o) {
+            const int qq = 4 * u + ee - o - 2;
+            if (qq >= 0 && qq < 29) acc[o] += ah[qq < 14 ? 14 - qq : qq - 14] * v.v[ee];
+          }
+      }
+      const int col = c0 + 4 * pg;
+      if (col < 7 || col + 4 * PQ - 1 >= n2 - 7) {  // the edge terms of the first / last 7 columns
+#pragma unroll
+        for (int o = 0; o < 4 * PQ; ++o) {
+          const int j = col + o;
+          if (j < 7) {
+            for (int c = 0; c < 7; ++c) acc[o] -= ehl[8 * j + c] * psrow[16 + c];
+          } else if (j >= n2 - 7 && j < n2) {
+            const int jj = j - (n2 - 7), s0 = n2 - 7 - c0 + 16;
+            for (int c = 0; c < 7; ++c) acc[o] -= ehh[8 * jj + c] * psrow[s0 + c];
+          }
+        }
+      }
+      int slot = (cur.s * RS) % RING + pr;
+      slot = slot >= RING ? slot - RING : slot;
+      T* dst = ring + slot * TP + 4 * pg;
+#pragma unroll
+      for (int k = 0; k < 4 * PQ / VN; ++k) {
+        V16<T> c;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) c.v[e] = acc[k * VN + e];
+        stv(dst + k * VN, c);
+      }
+      if (slot < G::MIR) {  // the ring's first RB + 27 rows again past its end
+#pragma unroll
+        for (int k = 0; k < 4 * PQ / VN; ++k) {
+          V16<T> c;
+#pragma unroll
+          for (int e = 0; e < VN; ++e) c.v[e] = acc[k * VN + e];
+          stv(dst + RING * TP + k * VN, c);
+        }
+      }
+    }
+    lds_barrier();
+    // ---- PV: out row i = a - 28 + s RS + r0 + rr reads t rows i - 14 .. i + 14 (staged s RS + r0 + rr - 28 ..)
+    {
+      const int base = (cur.s * RS + r0 - 28 + RING) % RING;
+      const T* rcol = ring + base * TP + VN * vg;  // window row j at rcol + j TP (contiguous: the mirror)
+      V16<T> acc[RB];
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int m = 0; m < VN; ++m) acc[rr].v[m] = T(0);
+      constexpr int NV = RB + 28, CH = 4, NCH = NV / CH;
+      static_assert(NV % CH == 0, "whole chunks");
+      V16<T> w[2][CH];  // chunk c in w[c & 1]; the next chunk's reads in flight during this one's FMAs
+      auto rd = [&](int c, V16<T>(&wc)[CH]) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          wc[j] = nrm_ldsv(rcol + (c * CH + j) * TP);
+        }
+      };
+      rd(0, w[0]);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) rd(c + 1, w[(c + 1) & 1]);
+        nrm_fence();
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int v = c * CH + j;
+#pragma unroll
+          for (int rr = 0; rr < RB; ++rr) {
+            const int qq = v - rr;
+            if (qq >= 0 && qq < 29) {
+              const T h = av[qq < 14 ? 14 - qq : qq - 14];
+#pragma unroll
+              for (int m = 0; m < VN; ++m) acc[rr].v[m] += h * w[c & 1][j].v[m];
+            }
+          }
+        }
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+          for (int m = 0; m < VN; ++m) asm volatile("" : "+v"(acc[rr].v[m]));
+        nrm_fence();
+      }
+      // every thread issues RB stores per step (rows outside [a, b) dropped by the range check),
+      // so the next step's wait for its staged rows leaves these stores in flight
+      const Rsrc dst = rsrc_of(out + cur.plane * (int64_t)n1 * n2, (uint32_t)((int64_t)n1 * n2 * sizeof(T)));
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr) {
+        const int i = cur.a - 28 + cur.s * RS + r0 + rr;
+        const bool live = i >= cur.a && i < cur.b && gc < n2;
+        if (live && (i < 7 || i >= n1 - 7)) {  // the edge terms of the first / last 7 rows
+          const bool top = i < 7;
+          const int jr = top ? i : i - (n1 - 7), row0 = top ? 0 : n1 - 7;
+          const T* e = top ? evl : evh;
+          for (int c = 0; c < 7; ++c) {
+            const V16<T> wv = ldv(ring + ((row0 + c - cur.a + 14) % RING) * TP + VN * vg);
+            const T ec = e[8 * jr + c];
+#pragma unroll
+            for (int m = 0; m < VN; ++m) acc[rr].v[m] -= ec * wv.v[m];
+          }
+        }
+        if constexpr (SUB) {
+#pragma unroll
+          for (int m = 0; m < VN; ++m) acc[rr].v[m] = acc[rr].v[m] - bsub[rr].v[m];
+        }
+        u4 d;
+        __builtin_memcpy(&d, acc[rr].v, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(d, dst, (int)(live ? (uint32_t)(((int64_t)i * n2 + gc) * sizeof(T)) : kOOB), 0, 0);
+      }
+    }
+  };
+  auto advance = [&](const Cur& c, bool& more) {  // the step after c (more = false: none)
     Cur n = c;
     more = true;
     if (c.s + 1 < c.ns) {
@@ -765,64 +979,43 @@ __global__ __launch_bounds__(NrmCfg<T>::G::NT, sizeof(T) == 4 ? 3 : 2) void k_se
     }
     return n;
   };
-  // two register sets, the rows of step k + 2 issued at step k's top: at a step's top its own loads,
-  // the previous two steps' stores and the next step's loads are in flight
-  Q4<T> qa[NL], qb[NL];
-  using W2 = std::integral_constant<int, NL + 2 * G::NST>;
-  Cur c0 = task_at(t0);
-  bool m1, m2, m3;
-  Cur c1 = advance(c0, m1);
-  prefetch(c0, qa);
-  prefetch(c1, qb);  // unconditional (re-reads c0's rows when there is no next step)
-  for (;;) {
-    stage(qa, W2{});
-    Cur c2 = c1;
-    m2 = false;
-    if (m1) c2 = advance(c1, m2);
-    issue(c2, qa);
-    body(c0);
-    if (!m1) break;
-    stage(qb, W2{});
-    Cur c3 = c2;
-    m3 = false;
-    if (m2) c3 = advance(c2, m3);
-    issue(c3, qb);
-    body(c1);
-    if (!m2) break;
-    c0 = c2;
-    c1 = c3;
-    m1 = m3;
-  }
-#else
   Q4<T> q[NL];
   Cur cur = task_at(t0);
   prefetch(cur, q);
   for (;;) {
-    // the previous step's RB row stores (4 / 8 dwordx4) may still be in flight
-    stage(q, std::integral_constant<int, G::NST>{});
-    Cur nxt = cur;
-    bool more = true;
-    if (cur.s + 1 < cur.ns) {
-      nxt.s = cur.s + 1;
-    } else {
-      more = cur.t + t_stride < t_end;
-      if (more) nxt = task_at(cur.t + t_stride);
-    }
-    issue(nxt, q);  // unconditional (the last step re-reads its own rows): the wait for these
-                    // loads at the next step then leaves this step's stores in flight
+    // the previous step's RB row stores may still be in flight (with SUB the wait also covers its RB
+    // sub loads, issued before the stores)
+    stage(q, std::integral_constant<int, RB>{});
+    bool more;
+    const Cur nxt = advance(cur, more);
+    prefetch(nxt, q);  // unconditional (the last step re-reads its own rows): the wait for these
+                       // loads at the next step then leaves this step's stores in flight
     body(cur);
     if (!more) break;
     cur = nxt;
   }
-#endif
 }
 
-template <typename T, bool SUB = false>
+// fp32: k_sep2d_nrm (53 KB of LDS, 3 workgroups / CU); fp64: k_sep2d_nrmm (77 KB, 2 / CU).  The mirrored ring
+// in fp32 needs 72 KB (2 / CU) and measured slower there: 512^3 0.41-0.48 against 0.36-0.43 ms, 4096^2 equal;
+// in fp64 it took 1024^3 from 5.19-5.22 to 4.59-4.67 ms, 4096^2 from 0.108-0.111 to 0.098-0.100 ms (bitwise the
+// same output; loading two steps ahead: no further change, profiles/r5_nrm_ab.txt)
+template <typename T, bool SUB>
+static const void* nrm_fn() {
+  if constexpr (sizeof(T) == 8) return reinterpret_cast<const void*>(&k_sep2d_nrmm<T, SUB>);
+  else return reinterpret_cast<const void*>(&k_sep2d_nrm<T, SUB>);
+}
+template <typename T>
+static size_t nrm_lds() {
+  if constexpr (sizeof(T) == 8) return NrmM<T>::lds_bytes();
+  else return NrmF::lds_bytes();
+}
+
+template <typename T, bool SUB>
 static void nrm_attr() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep2d_nrm<T, SUB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)NrmCfg<T>::G::lds_bytes());
+    (void)hipFuncSetAttribute(nrm_fn<T, SUB>(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)nrm_lds<T>());
     (void)hipGetLastError();
     done = true;
   }
@@ -832,13 +1025,12 @@ template <typename T>
 static int nrm_slots() {
   static int slots = 0;
   if (slots == 0) {
-    using G = typename NrmCfg<T>::G;
     int dev = 0, cus = 0, nb = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                 hipSuccess || cus < 1)
       cus = 256;
-    nrm_attr<T>();
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sep2d_nrm<T, false>, G::NT, G::lds_bytes()) != hipSuccess ||
+    nrm_attr<T, false>();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nrm_fn<T, false>(), 256, nrm_lds<T>()) != hipSuccess ||
         nb < 1)
       nb = 1;
     (void)hipGetLastError();
@@ -860,9 +1052,9 @@ static bool nrm_fits(int64_t n1, int64_t n2, int ka, int offa, int kb, int offb)
 template <typename T>
 static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2, const void* ha, int ka, int offa,
                    const void* hb, int kb, int offb, hipStream_t st, const void* sub = nullptr) {
-  using G = typename NrmCfg<T>::G;
+  constexpr int TX = sizeof(T) == 8 ? NrmM<T>::TX : NrmF::TX;
   if (np == 0) return PCS_OK;
-  const int64_t nstrips = (n2 + G::TX - 1) / G::TX, pieces = np * nstrips;
+  const int64_t nstrips = (n2 + TX - 1) / TX, pieces = np * nstrips;
   const int64_t slots = nrm_slots<T>();
   // row segments: the fewest (each task re-reads a 28-row prologue) whose tasks fill the resident
   // workgroup slots once, segments of >= 64 rows; then one task per workgroup, later workgroups
@@ -884,16 +1076,20 @@ static int sep_nrm(const void* in, void* out, int64_t np, int64_t n1, int64_t n2
   }
   const int64_t gslots = gridx > 0 ? slots * gridx : ntasks;
   const int64_t grid = ntasks < gslots ? ntasks : gslots;
+  const size_t lds = nrm_lds<T>();
+  auto go = [&](auto kern) {
+    kern<<<(unsigned)grid, 256, lds, st>>>((const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg,
+                                           (int)seg_len, ntasks, (const T*)ha, ka, offa, (const T*)hb, kb, offb,
+                                           (const T*)sub);
+  };
   if (sub != nullptr) {
     nrm_attr<T, true>();
-    k_sep2d_nrm<T, true><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>(
-        (const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg, (int)seg_len, ntasks, (const T*)ha, ka, offa,
-        (const T*)hb, kb, offb, (const T*)sub);
+    if constexpr (sizeof(T) == 8) go(k_sep2d_nrmm<T, true>);
+    else go(k_sep2d_nrm<T, true>);
   } else {
-    nrm_attr<T>();
-    k_sep2d_nrm<T, false><<<(unsigned)grid, G::NT, G::lds_bytes(), st>>>(
-        (const T*)in, (T*)out, (int)n1, (int)n2, (int)nstrips, (int)nseg, (int)seg_len, ntasks, (const T*)ha, ka, offa,
-        (const T*)hb, kb, offb, nullptr);
+    nrm_attr<T, false>();
+    if constexpr (sizeof(T) == 8) go(k_sep2d_nrmm<T, false>);
+    else go(k_sep2d_nrm<T, false>);
   }
   return launch_status();
 }

@@ -285,12 +285,6 @@ class PDS2DEngine:
         # host cost is far below the step, and back-to-back launches measured faster than
         # replaying a captured graph of the same launches; small images keep the graph
         self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
-        # PCS_PERSISTENT=1: a native chunk is ONE launch with a grid barrier per iteration
-        # (pcs_pds2d_run_persistent; pointwise-F family only, else the back-to-back launches)
-        self.persistent = self.native and os.environ.get('PCS_PERSISTENT', '0') == '1'
-        self.bar = None
-        if self.persistent:
-            self.bar = torch.zeros(int(self.lib.pcs_grid_bar_bytes()) // 4, dtype=torch.int32, device=dev)
 
     def _bind(self, a, p):
         """Point the step's iterate buffers at parity p (reads buffers p, writes 1 - p)."""
@@ -341,18 +335,7 @@ class PDS2DEngine:
         a = self.args
         self._bind(a, 0)
         a.hist = hist.data_ptr()
-        if self.persistent:
-            rc = self.lib.pcs_pds2d_run_persistent(ctypes.byref(a), self.chunk, L.ptr(self.bar), L.stream())
-            if rc == 0:
-                return
-            if rc != -3:
-                L.check(rc, 'pcs_pds2d_run_persistent')
-            self.persistent = False  # not applicable to this problem
         self._run_call(self.chunk)
-
-    def barrier_timed_out(self):
-        """True if a persistent launch's grid barrier gave up (grid not co-resident)."""
-        return self.bar is not None and int(self.bar[64].item()) != 0
 
     # ---- fixed-count loop for benchmarking (bench.py): no early stop, optional per-step events
     def prepare_fixed(self, total_iters, chunk):
@@ -497,7 +480,7 @@ class PDS2DEngine:
                 pending.append(ev)
                 if len(pending) >= 2:
                     pending.pop(0).synchronize()
-                    if int(self.ctrl_host[1]) != 0 or (self.persistent and self.barrier_timed_out()):
+                    if int(self.ctrl_host[1]) != 0:
                         break
         else:
             for k in range(n_chunks):
@@ -507,11 +490,6 @@ class PDS2DEngine:
                     break
         hist = self.hist
         torch.cuda.synchronize()
-        if self.persistent and self.barrier_timed_out():
-            # a persistent chunk's grid barrier gave up: x / z hold a mix of iterations and the
-            # loop control is inconsistent -- never return that as a result
-            raise RuntimeError('pcs_pds2d_run_persistent: grid barrier timed out (workgroups not co-resident); '
-                               'rerun without PCS_PERSISTENT=1')
         c = self.ctrl.view(torch.int32)[:2].cpu().numpy()
         n = int(c[0])
         h = hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
@@ -629,7 +607,6 @@ class PDS2DStencilEngine(PDS2DEngine):
         self.hist = None
         self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
         self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
-        self.persistent = False
         self.bar = None
 
     def time_iteration_kernels(self, n):
@@ -763,7 +740,6 @@ class PDS2DMaskEngine(PDS2DEngine):
         self.hist = None
         self.ctrl_host = torch.zeros(2, dtype=torch.int32).pin_memory()
         self.native = self.N >= NATIVE_MIN_PIXELS
-        self.persistent = False
         self.bar = None
 
     def _bind(self, a, p):

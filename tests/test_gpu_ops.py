@@ -591,24 +591,3 @@ def test_convolve1d_lipschitz_doctest(A):
     np.testing.assert_array_equal(np.round(op.singularvals(k=3, which='LM', tol=1e-3), 2), [0.5, 0.5, 0.5])
     op.compute_lipschitz_cst(tol=1e-2)
     assert np.round(op.lipschitz_cst, 1) == 0.5
-
-
-@pytest.mark.parametrize('k', [3, 7, 15, 31])
-@pytest.mark.parametrize('shape', [(517, 1023), (130, 64), (64, 4096)])
-def test_corr2d_packed_matches_scalar(A, k, shape, monkeypatch):
-    """The fp32 packed correlation kernel (k_corr2d_pk: two output rows per v_pk_fma_f32, opt-in
-    PCS_CORR_PK=1) against the scalar kernel (the default): each lane runs the scalar kernel's fmaf
-    sequence, so the outputs are equal (forward with the fused residual, adjoint)."""
-    from pycsou_amd.linop.conv import Convolve2D
-    rng = np.random.default_rng(k)
-    h = rng.standard_normal((k, k))
-    N = shape[0] * shape[1]
-    x = dev(rng.standard_normal(N).astype(np.float32))
-    y = dev(rng.standard_normal(N).astype(np.float32))
-    op = Convolve2D(N, h, shape)
-    outs = {}
-    for pk in ('1', '0'):
-        monkeypatch.setenv('PCS_CORR_PK', pk)
-        outs[pk] = (op._apply_minus(x, y).clone(), op._adj(x).clone())
-    assert torch.equal(outs['1'][0], outs['0'][0])
-    assert torch.equal(outs['1'][1], outs['0'][1])

@@ -593,32 +593,6 @@ def test_rccl_transport_graph_capture_world1():
     assert lib.pcs_comm_destroy(h) == 0
 
 
-@pytest.mark.parametrize('shape, thr', [((700, 256), 2e-3), ((1100, 1000), 0.0)])
-def test_persistent_loop_matches_launches(monkeypatch, shape, thr):
-    """pcs_pds2d_run_persistent (one launch per chunk, a grid barrier per iteration) against
-    pcs_pds2d_run (one launch per iteration): same exit iteration, x and z bitwise, history to
-    1e-5 (the persistent grid may group the partials differently)."""
-    from pycsou_amd.opt import engine as E
-    monkeypatch.setattr(E, 'NATIVE_MIN_PIXELS', 1)
-    pds = _denoise_problem(*shape, thr=thr, max_iter=60 if thr == 0 else 400, min_iter=5)
-    spec = pds._fused_spec()
-    mi = 60 if thr == 0 else 400
-    monkeypatch.setenv('PCS_PERSISTENT', '0')
-    e1 = E.PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, chunk=16)
-    assert e1.native and not e1.persistent
-    n, x1, z1, h1 = e1.run(mi, 5, thr)
-    monkeypatch.setenv('PCS_PERSISTENT', '1')
-    e2 = E.PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, chunk=16)
-    assert e2.persistent
-    n2, x2, z2, h2 = e2.run(mi, 5, thr)
-    assert e2.persistent, 'persistent launch was not applicable'
-    assert not e2.barrier_timed_out()
-    assert n2 == n and (thr == 0 or 6 < n < 400)
-    assert torch.equal(x2, x1) and torch.equal(z2, z1)
-    k = 2 * n
-    assert np.allclose(h2[1:k], h1[1:k], rtol=1e-5)
-
-
 def test_pds3d_capture_failure_falls_back_to_eager(monkeypatch):
     """A library error (HipError) raised while a chunk is being captured leaves the 3-D engine on
     eager launches (the capture outcome is agreed collectively, so every rank must get past the
