@@ -511,11 +511,15 @@ def leg_c3_f64(args, dtype, K, W, kind='forward'):
     alg = 7 * N * 8
     km = r['kernels_ms']
     sub = os.environ.get('PCS_NX_SUB', '1') != '0'
+    fused = 'conv_nx' not in km
     res = {'workload': f'C3 TV-deconvolution {n}x{n} f64 (the reference default dtype), 15x15 Gaussian PSF (separable), '
                        f'K = Gradient(kind={kind}), 0.05*L21Norm; grad F = N x - Conv^T y: '
-                       + ('grad F by k_sep2d_nrm<double> (N x minus Conv^T y as it stores) into a buffer'
-                          if sub else 'N x by k_sep2d_nrm<double> into a buffer')
-                       + ' + the fp64 general-stencil march step (k_pds2d_smarch<double>), back to back from C',
+                       + ('N inside the step, ONE launch per iteration (k_pds2d_nmarch64, the fused fp64 '
+                          'normal-operator march)' if fused else
+                          ('grad F by k_sep2d_nrmm<double> (N x minus Conv^T y as it stores) into a buffer'
+                           if sub else 'N x by k_sep2d_nrmm<double> into a buffer')
+                          + ' + the fp64 general-stencil march step (k_pds2d_smarch<double>)')
+                       + ', back to back from C',
            'it_per_s': round(1e3 / r['ms_per_step'], 1), 'ms_per_iter': round(r['ms_per_step'], 5),
            'steps': K, 'warmup': W, 'setup_s': round(setup, 2), 'dtype': 'f64',
            'kernels_ms': {k: round(v, 5) for k, v in km.items()}, 'alg_bytes_per_iter': alg,
@@ -529,10 +533,17 @@ def leg_c3_f64(args, dtype, K, W, kind='forward'):
                            'kernel_ms': round(upd, 5), 'bytes_per_launch': step_bytes,
                            'achieved': round(step_bytes / (upd * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                            'frac': round(step_bytes / (upd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        res['nx_roofline'] = {'bound': 'hbm', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrm<double>, timed alone)',
+        res['nx_roofline'] = {'bound': 'hbm', 'kernel': 'pcs_conv2d_sep_ata_planes (k_sep2d_nrmm<double>, timed alone)',
                               'kernel_ms': round(km['conv_nx'], 5), 'bytes_per_launch': 2 * N * 8,
                               'achieved': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9, 1),
                               'frac': round(2 * N * 8 / (km['conv_nx'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    else:
+        res['roofline'] = {'bound': 'hbm', 'kernel': f'pcs_pds2d_step (k_pds2d_nmarch64<7, L21, {kind}>)',
+                           'kernel_ms': round(km['step'], 5), 'bytes_per_launch': alg,
+                           'achieved': round(alg / (km['step'] * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': round(alg / (km['step'] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           'conv_flop_per_launch': 116 * N,
+                           'conv_tflops_fp64': round(116 * N / (km['step'] * 1e-3) / 1e12, 2)}
     return res
 
 

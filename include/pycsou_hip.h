@@ -304,6 +304,19 @@ typedef struct {
 enum { PCS_M_NONE = 0, PCS_M_L1LOSS = 1 };
 /* 1 if pcs_pds2d_step runs these arguments (0: PCS_EUNSUPPORTED / invalid). */
 int pcs_pds2d_supported(const pcs_pds2d_args* a);
+/* Which kernel family pcs_pds2d_step runs for these arguments (-1: none), so an engine can tell the fused
+ * normal-operator marches (one launch per iteration) from the split forms: */
+enum {
+  PCS_PATH_TILE = 1,      /* the tile kernel (pds_tile.hpp)                                         */
+  PCS_PATH_MARCH = 2,     /* fp32 separable PSF, four-pass row march (pds_march.hpp)                */
+  PCS_PATH_NMARCH = 3,    /* fp32 separable PSF, normal-operator march (pds_nmarch.hpp)             */
+  PCS_PATH_PT = 4,        /* fp32 pointwise grad F, forward K (pds_pt.hpp)                          */
+  PCS_PATH_SMARCH = 5,    /* general-stencil march, pointwise grad F (pds_smarch.hpp)               */
+  PCS_PATH_SMARCH_NX = 6, /* N x pass into gbuf, then the general-stencil march (two launches)      */
+  PCS_PATH_NM64 = 7,      /* fp64 separable PSF, fused normal-operator march (pds_nm64.hip)         */
+  PCS_PATH_CONV2D = 8     /* two correlation passes, then the step with grad F from gbuf            */
+};
+int pcs_pds2d_path(const pcs_pds2d_args* a);
 int pcs_pds2d_ntaps_len(int half); /* 64 + 32 * tier(half); -1 beyond tier 7 */
 
 int pcs_pds2d_halo_x(int half);

@@ -22,6 +22,10 @@ PCS_G_NULL, PCS_G_NONNEG, PCS_G_SEGMENT = 0, 1, 2
 PCS_APGD_G_L1 = 3
 PCS_F_NULL, PCS_F_DENOISE, PCS_F_SEPCONV, PCS_F_GRADBUF, PCS_F_CONV2D, PCS_F_CONV0 = 0, 1, 2, 3, 4, 5
 PCS_M_NONE, PCS_M_L1LOSS = 0, 1
+# pcs_pds2d_path: the kernel family of a fused 2-D step
+(PCS_PATH_TILE, PCS_PATH_MARCH, PCS_PATH_NMARCH, PCS_PATH_PT, PCS_PATH_SMARCH, PCS_PATH_SMARCH_NX, PCS_PATH_NM64,
+ PCS_PATH_CONV2D) = range(1, 9)
+PCS_PATH_FUSED_NORMAL = (PCS_PATH_NMARCH, PCS_PATH_NM64)  # grad F = N x - Conv^T y inside the one launch
 KINDS = {'forward': PCS_FORWARD, 'backward': PCS_BACKWARD, 'centered': PCS_CENTERED}
 
 _c_int, _c_i64, _c_dbl, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -134,6 +138,7 @@ _SIGS = {
     'pcs_fftconv2d_apply': (_c_int, [_vp, _vp, _vp, _c_int, _vp, _c_dbl, _vp]),
     'pcs_fftconv2d_destroy': (_c_int, [_vp]),
     'pcs_pds2d_supported': (_c_int, [ctypes.POINTER(PdsArgs)]),
+    'pcs_pds2d_path': (_c_int, [ctypes.POINTER(PdsArgs)]),
     'pcs_pds2d_run': (_c_int, [ctypes.POINTER(PdsArgs), _c_i64, _vp]),
     'pcs_pds2d_stencil_nblocks': (_c_i64, [ctypes.POINTER(StencilArgs)]),
     'pcs_pds2d_stencil_ws_bytes': (_c_i64, [ctypes.POINTER(StencilArgs)]),

@@ -165,6 +165,7 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 // the row-marching families (march, pt, smarch) take row bands; the tile kernel runs whole slabs only
 static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
+  if (use_nm64(a)) return launch_nmarch64(a, rb, st);
   if (use_smarch(a)) return a->dtype == PCS_F64 ? sm_launch<double>(a, rb, st) : sm_launch<float>(a, rb, st);
   if (use_march(a)) return launch_march(a, rb, st);
   if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
@@ -175,7 +176,7 @@ static int pds2d_bands(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
 
 template <typename T>
 static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
-  if (use_smarch(a) || use_march(a)) return pds2d_bands(a, full_bands(a), st);
+  if (use_nm64(a) || use_smarch(a) || use_march(a)) return pds2d_bands(a, full_bands(a), st);
   if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
   if (use_pt(a)) return pds2d_bands(a, full_bands(a), st);
   switch (a->fkind) {
@@ -196,6 +197,10 @@ static int pds2d(const pcs_pds2d_args* a, hipStream_t st) {
 
 static int64_t bands_nblocks(const pcs_pds2d_args* a, RowBands rb) {
   MarchPlan p;
+  if (use_nm64(a)) {
+    nm64_plan(a, rb, &p);
+    return (int64_t)p.ntasks;
+  }
   if (use_smarch(a)) {
     sm_plan(a, rb, &p);
     return (int64_t)p.ntasks;
@@ -260,7 +265,7 @@ int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a) {
     return pcs_pds2d_nblocks(&b);
   }
   if (!a || a->rows < 1 || a->n1 < 1) return -1;
-  if (use_smarch(a) || a->kkind != PCS_K_GRAD_FORWARD) return bands_nblocks(a, full_bands(a));
+  if (use_nm64(a) || use_smarch(a) || a->kkind != PCS_K_GRAD_FORWARD) return bands_nblocks(a, full_bands(a));
   if (use_march(a) || use_pt(a)) return bands_nblocks(a, full_bands(a));
   const int th = a->dtype == PCS_F64 ? Tile<double>::TH : Tile<float>::TH;
   return ((a->n1 + 63) / 64) * ((a->rows + th - 1) / th);
@@ -326,7 +331,8 @@ int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int6
   if (rc != PCS_OK) return rc;
   if (a->hist || !bands_ok(a, ra0, rb0, ra1, rb1)) return PCS_EINVAL;
   if (a->fkind == PCS_F_CONV2D) return PCS_EUNSUPPORTED;  // its correlation passes run once per iteration
-  if (!(use_smarch(a) || use_march(a) || (a->kkind == PCS_K_GRAD_FORWARD && use_pt(a)))) return PCS_EUNSUPPORTED;
+  if (!(use_nm64(a) || use_smarch(a) || use_march(a) || (a->kkind == PCS_K_GRAD_FORWARD && use_pt(a))))
+    return PCS_EUNSUPPORTED;
   return pds2d_bands(a, RowBands{ra0, rb0, ra1, rb1}, st);
 }
 
@@ -336,9 +342,23 @@ int pcs_pds2d_supported(const pcs_pds2d_args* a) {
     const pcs_pds2d_args b = step_args(a);
     return pcs_pds2d_supported(&b);
   }
-  if (a->kkind != PCS_K_GRAD_FORWARD) return (use_smarch(a) || use_march(a)) ? 1 : 0;
-  if (use_smarch(a) || use_march(a) || use_pt(a)) return 1;
+  if (a->kkind != PCS_K_GRAD_FORWARD) return (use_nm64(a) || use_smarch(a) || use_march(a)) ? 1 : 0;
+  if (use_nm64(a) || use_smarch(a) || use_march(a) || use_pt(a)) return 1;
   return (a->dtype == PCS_F32 || a->dtype == PCS_F64) && (a->fkind != PCS_F_SEPCONV || tier_for(a->half) > 0) ? 1 : 0;
+}
+
+int pcs_pds2d_path(const pcs_pds2d_args* a) {
+  if (check_args(a) != PCS_OK) return -1;
+  if (a->fkind == PCS_F_CONV2D) {
+    const pcs_pds2d_args b = step_args(a);
+    return pcs_pds2d_supported(&b) ? PCS_PATH_CONV2D : -1;
+  }
+  if (use_nm64(a)) return PCS_PATH_NM64;
+  if (use_smarch(a)) return a->fkind == PCS_F_SEPCONV ? PCS_PATH_SMARCH_NX : PCS_PATH_SMARCH;
+  if (use_march(a)) return use_nmarch(a) ? PCS_PATH_NMARCH : PCS_PATH_MARCH;
+  if (a->kkind != PCS_K_GRAD_FORWARD) return -1;
+  if (use_pt(a)) return PCS_PATH_PT;
+  return pcs_pds2d_supported(a) ? PCS_PATH_TILE : -1;
 }
 
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t st) {

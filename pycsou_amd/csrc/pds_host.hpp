@@ -158,6 +158,33 @@ static bool sm_forward() {
 
 static int sm_slots_for(const pcs_pds2d_args* a) { return a->dtype == PCS_F64 ? sm_slots<double>() : sm_slots<float>(); }
 
+// the fused fp64 normal-operator march (pds_nm64.hip): fp64, separable PSF of tier 3 / 7 with the host's
+// Conv^T y and fp64 N tables, Gradient K of any kind, H = lam L1 / L21; PCS_NM64=0 (read per call): the split
+// form (N x by k_sep2d_nrmm into the gradient buffer, then the stencil march)
+int nm64_slots();
+bool nm64_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p);
+int launch_nmarch64(const pcs_pds2d_args* a, RowBands rb, hipStream_t st);
+static bool use_nm64(const pcs_pds2d_args* a) {
+  const char* e = getenv("PCS_NM64");
+  if (e != nullptr && atoi(e) == 0) return false;
+  if (a->dtype != PCS_F64 || a->fkind != PCS_F_SEPCONV || a->mkind != PCS_M_NONE) return false;
+  if (!a->cty || !a->ntaps || !aligned16(a->cty) || a->half < 0) return false;
+  if (a->kkind != PCS_K_GRAD_FORWARD && a->kkind != PCS_K_GRAD_BACKWARD && a->kkind != PCS_K_GRAD_CENTERED) return false;
+  if (a->hkind != PCS_H_L1 && a->hkind != PCS_H_L21) return false;
+  const int t = tier_for(a->half);
+  if ((t != 3 && t != 7) || !make_slab(a).vec || a->n0 < 64 || a->n1 < 128) return false;
+  // slabs: x rows 2H + 1 past the own rows (the PV windows of the U rows one past them), b one, z one
+  // (forward K) / two
+  if (a->rows < a->n0 &&
+      (a->halo_x < 2 * t + 1 || a->halo_y < 1 || a->halo_z < (a->kkind == PCS_K_GRAD_FORWARD ? 1 : 2)))
+    return false;
+  const int64_t hmax = a->halo_x > a->halo_z ? (a->halo_x > a->halo_y ? a->halo_x : a->halo_y)
+                                             : (a->halo_z > a->halo_y ? a->halo_z : a->halo_y);
+  if (!(a->n0 < (1LL << 30) && (a->rows + 2 * hmax) * a->n1 * 8 <= (1LL << 30))) return false;
+  MarchPlan p;
+  return nm64_plan(a, full_bands(a), &p);
+}
+
 static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tiles_x = (int)((a->n1 + 63) / 64);
   if (tiles_x < 2) return false;

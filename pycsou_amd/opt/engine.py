@@ -91,7 +91,7 @@ def _match_h(H, ncomp, N):
     return None
 
 
-def nmarch_taps(t0, t1, half):
+def nmarch_taps(t0, t1, half, dtype=np.float32):
     """The N = Conv^T Conv tables of the normal-operator march kernel (pds_nmarch.hpp) for a
     separable PSF with centred taps t0 (axis 0) and t1 (axis 1) of half width `half`, padded to
     the tier H (3 or 7): (Conv v)[i] = sum_d c[d] v[i - d], c[d] = t[H + d].  Away from the
@@ -99,7 +99,8 @@ def nmarch_taps(t0, t1, half):
     q = 0..4H); on the H samples nearest each edge the zero boundary removes the terms of the
     samples outside the image: N[j, k] = a[j - k] - E[j][k], E[j][k] = sum_{i < 0} c[i - j] c[i - k]
     (left / top, j, k < H) and the mirror sum over i >= n on the right / bottom.  Computed in fp64,
-    returned as the fp32 layout the kernel reads (64 + 32 H values)."""
+    returned in the layout the kernels read (64 + 32 H values) as `dtype` (the fp32 march: float32; the
+    fp64 march, pds_nm64.hip: float64)."""
     H = 3 if half <= 3 else 7
     out = np.zeros(64 + 32 * H)
 
@@ -130,7 +131,7 @@ def nmarch_taps(t0, t1, half):
         for cc in range(H):
             out[base + 16 * H + 8 * k + cc] = eh_lo[cc][k]
             out[base + 24 * H + 8 * k + (8 - H) + cc] = eh_hi[cc][k]
-    return out.astype(np.float32)
+    return out.astype(dtype)
 
 
 def match_stencil2d(F, G, H, K, has_H):
@@ -560,15 +561,16 @@ class PDS2DStencilEngine(PDS2DEngine):
                     a.fkind, a.half, a.y = L.PCS_F_SEPCONV, half, self.y.data_ptr()
                     a.taps0, a.taps1 = self.taps[0].data_ptr(), self.taps[1].data_ptr()
                     a.cty = self.cty.data_ptr()
-                    # the N tables: backward / centred K take the fused normal-operator march (one
-                    # launch, pds_nmarch.hpp, fp32) when the library does -- supported with no gradient
-                    # buffer; fp64 takes the two-launch form (N x by k_sep2d_nrm, then the march step)
-                    self.nm_fused = False
-                    if not f64:
-                        self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
-                        a.ntaps = self.ntaps.data_ptr()
-                        a.gbuf = None
-                        self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+                    # the N tables: the fused normal-operator march (one launch: pds_nmarch.hpp for
+                    # backward / centred K in fp32, pds_nm64.hip for every Gradient K in fp64) when the
+                    # library takes the problem -- supported with no gradient buffer; otherwise the
+                    # two-launch form (N x by the in-plane normal-operator kernel, then the march step)
+                    self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half, np.float64 if f64 else np.float32)).to(dev)
+                    a.ntaps = self.ntaps.data_ptr()
+                    a.gbuf = None
+                    self.nm_fused = self.lib.pcs_pds2d_path(ctypes.byref(a)) in L.PCS_PATH_FUSED_NORMAL
+                    if not self.nm_fused:
+                        a.ntaps = None
                     a.gbuf = gsrc.data_ptr()
                     if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
                         a.fkind, a.cty, a.ntaps = fk, None, None

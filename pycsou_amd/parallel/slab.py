@@ -334,9 +334,10 @@ class SlabPDS2D:
         conv = spec.get('conv')
         if fk in (L.PCS_F_SEPCONV, L.PCS_F_GRADBUF) and conv is not None:
             sep = conv.separable(rtol=2e-7 if dtype == torch.float32 else 1e-13)
-            if sep is not None and (fwd or (dtype == torch.float32 and sep[2] <= 7)):
-                # forward K: the (normal-operator) march kernels; other K: N x by the in-plane
-                # normal-operator pass into a buffer, then the general-stencil march step
+            if sep is not None and (fwd or sep[2] <= 7):
+                # forward K: the (normal-operator) march kernels; other K: the fused normal-operator
+                # march (fp32 pds_nmarch.hpp, fp64 pds_nm64.hip) or N x by the in-plane normal-operator
+                # pass into a buffer, then the general-stencil march step
                 mode = 'sep' if fwd else 'sep_normal'
                 t0, t1, half = sep
                 self.taps = [torch.as_tensor(t0).to(device=dev, dtype=dtype),
@@ -386,26 +387,28 @@ class SlabPDS2D:
         if mode == 'conv2d':
             self.R = torch.zeros_like(self.X[0])
             a.rbuf = self.R.data_ptr()
-        if mode == 'sep_normal' or (mode == 'sep' and dtype == torch.float32 and half <= 7
-                                    and os.environ.get('PCS_NMARCH', '1') != '0'):
+        f64 = dtype == torch.float64
+        if mode == 'sep_normal' or (mode == 'sep' and half <= 7 and os.environ.get('PCS_NMARCH', '1') != '0'):
             # Conv^T y in fp64 on this rank's window only (own rows + the y halo), from the y rows
             # within the PSF's reach of it -- exact, since the sub-image's zero boundary falls where
             # the image's does or beyond the reach
-            if mode == 'sep' or (dtype == torch.float32 and half <= 7):
+            if half <= 7:
                 # 'sep_normal' too: backward / centred K run the fused normal-operator march when the
-                # library takes it (no N x pass, no gradient buffer read)
-                self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half)).to(dev)
+                # library takes it (no N x pass, no gradient buffer read); fp64 every Gradient K
+                # (pds_nm64.hip, its N tables in fp64)
+                self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half, np.float64 if f64 else np.float32)).to(dev)
                 a.ntaps = self.ntaps.data_ptr()
             self.cty = self._cty_window(spec, hy).to(dtype).contiguous()
             a.cty = self.cty.data_ptr()
         self.nm_fused = False
-        if mode == 'sep_normal' and getattr(self, 'ntaps', None) is not None:
-            # supported without the gradient buffer = the fused march (the iterate pointers are bound
-            # per parity later: placeholders for the query, never written)
+        if mode in ('sep_normal', 'sep') and getattr(self, 'ntaps', None) is not None:
+            # the fused normal-operator march (one launch, no gradient buffer) when the library runs it
+            # for these arguments (the iterate pointers are bound per parity later: placeholders for the
+            # query, never written)
             saved = (a.gbuf, a.x, a.xn, a.z, a.zn, a.partials)
             ph = self.X[0].data_ptr()
             a.gbuf, a.x, a.xn, a.z, a.zn, a.partials = None, ph, ph, ph, ph, ph
-            self.nm_fused = self.lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
+            self.nm_fused = self.lib.pcs_pds2d_path(ctypes.byref(a)) in L.PCS_PATH_FUSED_NORMAL
             a.gbuf, a.x, a.xn, a.z, a.zn, a.partials = saved
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
         if self.nblocks < 0:

@@ -23,6 +23,8 @@ SYNTH = {
     'nonsep_fwd_f32': ((140, 256), 'forward', 'l1', 'nonsep9', np.float32),
     'nonsep_cen_f32': ((200, 192), 'centered', 'l21', 'nonsep9', np.float32),
     'sep_cen_f32': ((240, 256), 'centered', 'l21', 'sep15', np.float32),
+    'sep_cen_f64': ((240, 256), 'centered', 'l21', 'sep15', np.float64),
+    'sep_fwd_f64': ((200, 320), 'forward', 'l1', 'sep15', np.float64),
 }
 
 

@@ -119,7 +119,7 @@ def _synth_single_and_slabs(name, world):
 
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('name', ['cen_denoise_f32', 'lap_denoise_f32', 'bwd_denoise_f32', 'nonsep_fwd_f64',
-                                  'nonsep_fwd_f32', 'nonsep_cen_f32', 'sep_cen_f32'])
+                                  'nonsep_fwd_f32', 'nonsep_cen_f32', 'sep_cen_f32', 'sep_cen_f64', 'sep_fwd_f64'])
 def test_slabs_general_k_and_conv_bitwise(name, world):
     """Row slabs of the general-stencil K (backward / centred Gradient, Laplacian: pds_smarch.hpp),
     of a non-separable PSF (grad F by two correlation passes over the stored rows inside the step,
@@ -127,27 +127,29 @@ def test_slabs_general_k_and_conv_bitwise(name, world):
     march step): x and z bitwise equal to the single-GPU engine, same iteration count."""
     (n1, x1, z1, h1), (n2, x2, z2, h2), slabs = _synth_single_and_slabs(name, world)
     assert n2 == n1 == 16
-    assert {s.mode for s in slabs} == {'conv2d' if 'nonsep' in name else 'sep_normal' if 'sep_' in name
-                                        else 'pointwise'}
+    assert {s.mode for s in slabs} == {'conv2d' if 'nonsep' in name else 'sep' if name == 'sep_fwd_f64'
+                                        else 'sep_normal' if 'sep_' in name else 'pointwise'}
     assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
     assert torch.equal(z2, z1), (z2 - z1).abs().max().item()
     assert np.allclose(h2[1:], h1[1:], rtol=1e-5)
-    if name == 'sep_cen_f32':  # the fused normal-operator march (pds_nmarch.hpp GEN) on the slabs too
+    if name in ('sep_cen_f32', 'sep_cen_f64', 'sep_fwd_f64'):  # the fused normal-operator march on the slabs too
         assert all(s.nm_fused for s in slabs)
 
 
-def test_slab_fused_normal_march_banded_bitwise():
-    """Separable PSF + centred K on the fused normal-operator march: the banded (boundary bands, then
-    interior) order on two slabs, bitwise the single-GPU engine."""
+@pytest.mark.parametrize('name', ['sep_cen_f32', 'sep_cen_f64', 'sep_fwd_f64'])
+def test_slab_fused_normal_march_banded_bitwise(name):
+    """Separable PSF on the fused normal-operator march (fp32 centred K: pds_nmarch.hpp; fp64 centred /
+    forward K: pds_nm64.hip): the banded (boundary bands, then interior) order on two slabs, bitwise the
+    single-GPU engine."""
     from pycsou_amd.parallel import SlabPDS2D, run_local
     from tests.slab_worker import synth_problem
-    pds = synth_problem('sep_cen_f32')
+    pds = synth_problem(name)
     pds.iterate()
     eng = pds._engine
     assert eng.nm_fused
     n1 = pds.iter
     x1, z1 = eng.X[n1 % 2].clone(), eng.Z[n1 % 2].clone()
-    pds2 = synth_problem('sep_cen_f32')
+    pds2 = synth_problem(name)
     slabs = [SlabPDS2D.from_pds(pds2, None, rank=r, world=2) for r in range(2)]
     assert all(s.nm_fused and s.overlap for s in slabs)
     res = run_local(slabs, pds2.max_iter, pds2.min_iter, pds2.accuracy_threshold, split=True)

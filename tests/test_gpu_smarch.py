@@ -194,8 +194,9 @@ def test_fused_normal_march_matches_two_launch(kind, monkeypatch):
 @pytest.mark.parametrize('case', range(len(CASES)), ids=lambda i: f'f64-{CASES[i][1]}-{CASES[i][0][0]}x{CASES[i][0][1]}')
 def test_smarch_fp64_vs_oracle(case):
     """The same cases in fp64 (the reference's default dtype: pycsou/opt/proxalgs.py:327,341,
-    linop/diff.py:777): the fp64 form of the row march for every K kind, the forward Gradient included,
-    and separable PSFs as N x by k_sep2d_nrm<double> + the march step.  Bar: x and z to 1e-10 relative,
+    linop/diff.py:777): the fp64 form of the row march for every K kind, the forward Gradient included;
+    separable PSFs through the fused fp64 normal-operator march (Gradient K) or N x by k_sep2d_nrmm + the
+    march step (Laplacian).  Bar: x and z to 1e-10 relative,
     both diagnostics columns to 1e-9 relative (fp64 against fp64: operation order only)."""
     from pycsou_amd import _lib as L
     shape, kind, hname, fk, gname, edge, steps, weights = CASES[case]
@@ -204,8 +205,8 @@ def test_smarch_fp64_vs_oracle(case):
     x, z, diag, eng = _fused(p, np.float64)
     assert eng.march, 'the fp64 row-marching kernel must take this problem'
     assert eng.args.dtype == L.PCS_F64
-    if fk.startswith('sep'):
-        assert eng.fkind == L.PCS_F_SEPCONV and eng.cty is not None and not eng.nm_fused
+    if fk.startswith('sep'):  # Gradient K: the fused fp64 march (pds_nm64.hip); Laplacian: N x + the march step
+        assert eng.fkind == L.PCS_F_SEPCONV and eng.cty is not None and eng.nm_fused == (kind != 'lap')
     assert x.dtype == np.float64
     assert rel(x, xr) < 1e-10, rel(x, xr)
     assert rel(z, zr) < 1e-10, rel(z, zr)
@@ -237,3 +238,4 @@ def test_fp64_default_routing_takes_the_march():
                   accuracy_threshold=0.0, verbose=None)
         pds.iterate()
         assert isinstance(pds._engine, PDS2DStencilEngine) and pds._engine.march, kind
+        assert pds._engine.nm_fused, kind  # one launch per iteration (pds_nm64.hip)
