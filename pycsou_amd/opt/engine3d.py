@@ -248,7 +248,9 @@ class PDS3DEngine:
         # from t = C12^T C12 x inside k_pds3d, whose second set of 512 threads keeps two 15-plane
         # register rings per voxel): 13 words per voxel and iteration instead of 15, bitwise the same
         # iterates; C4 1.63-1.65 ms against 1.72-1.74 ms with the separate pass
-        # (profiles/r3_ck30_fold_ab.txt).  PCS_3D_FOLD=0 keeps the separate pass.
+        # (profiles/r3_ck30_fold_ab.txt).  PCS_3D_FOLD=0 keeps the separate pass.  (Backward / centred K:
+        # the rings fit only beside 8-row k_pds3d_gen tiles, which cost more than the pass saves --
+        # profiles/r5_c4cen_fold_ab.txt.)
         self.fold = False
         if self.ata and self.kkind == L.PCS_FORWARD and os.environ.get('PCS_3D_FOLD', '1') != '0':
             _, h0, _, k0, off0 = self.ax0
@@ -262,6 +264,13 @@ class PDS3DEngine:
                 a.fkind, a.g, a.conv0_w, a.conv0_taps, a.conv0_k, a.conv0_off = (b.fkind, b.g, b.conv0_w,
                                                                                  b.conv0_taps, b.conv0_k, b.conv0_off)
                 self.fold = True
+                # the per-workgroup partials and the reduction workspace follow the folded launch's grid
+                self.nblocks = int(self.lib.pcs_pds3d_nblocks(ctypes.byref(a)))
+                self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
+                a.partials = self.partials.data_ptr()
+                self.ws = torch.zeros(int(self.lib.pcs_pds3d_ws_bytes(ctypes.byref(a))) // 8 + 2, dtype=torch.float64,
+                                      device=dev)
+                a.ws = self.ws.data_ptr()
         self.args = [self._args_for(p) for p in (0, 1)]
         self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)

@@ -434,7 +434,7 @@ def test_pds3d_gradient_order_default(monkeypatch, dtype, ata):
     assert rel(est['dual_variable'], z_ref) < tol
 
 
-@pytest.mark.parametrize('shape', [(24, 20, 24), (40, 24, 136), (17, 9, 132)])
+@pytest.mark.parametrize('shape', [(24, 20, 24), (40, 24, 136), (17, 9, 132), (23, 37, 260)])
 def test_pds3d_folded_axis0_bitwise(monkeypatch, shape):
     """fp32 forward K: the axis-0 pass folded into k_pds3d (PCS_F_CONV0, register rings of t and
     the residual) computes k_conv0_rta's sums in its order, so the iterates equal the separate
