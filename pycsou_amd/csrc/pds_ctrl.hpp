@@ -45,7 +45,14 @@ __device__ __forceinline__ void finalize_from(const double* v, Ctrl* c, double* 
 // finalize_from.  Fixed summation order => bitwise-reproducible diagnostics.
 // Workspace layout: [ngroups][4] doubles (group sums) | (ngroups + 1) uint32 counters,
 // zeroed once before first use; every counter is reset by its last arriver.
-constexpr int kGrp = 64;
+// workgroups per group (diagnostics builds override: PCS_RED_GRP).  1024: the one-round grids of the 2-D
+// marches (<= 1024 workgroups) reduce in a single level -- one counter round trip and one load round trip at
+// the end of the launch instead of two of each: 2048^2 stencil march 28.9-29.5 against 30.0-31.0 us, CPS
+// inpainting +5 % (profiles/r5_red_grp_ab.txt); 64 before
+#ifndef PCS_RED_GRP
+#define PCS_RED_GRP 1024
+#endif
+constexpr int kGrp = PCS_RED_GRP;
 
 __host__ __device__ inline int64_t red_groups(int64_t nblocks) { return (nblocks + kGrp - 1) / kGrp; }
 __host__ __device__ inline int64_t red_ws_bytes(int64_t nblocks) {
@@ -99,9 +106,14 @@ __device__ __forceinline__ bool stop_requested(const Ctrl* ctrl, const RedOut& r
 // Called by every thread of every workgroup after thread 0's `part` holds the block sums.
 // `flag` is a 2-int LDS scratch.  With ro.sums the last group writes the sums instead of
 // running finalize_from.
+// ablation (timing only, the loop control never advances; PCS_LIB_PATH builds): 1 = no reduction at all
+#ifndef PCS_RED_ABL
+#define PCS_RED_ABL 0
+#endif
 __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], double* __restrict__ partials,
                                                     int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag,
                                                     RedOut ro = RedOut{nullptr, nullptr, 0}) {
+  if (PCS_RED_ABL & 1) return;
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t ngr = red_groups(nblocks);
@@ -116,15 +128,35 @@ __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], dou
   }
   __syncthreads();
   if (!flag[0]) return;  // uniform
-  // ---- last workgroup of its group: lane j sums member j (wave-order reduction)
-  if (tid < 64) {
+  __shared__ double red2[4 * 16];
+  // ---- last workgroup of its group: thread j sums members j, j + blockDim, ... (fixed order), then the
+  // workgroup tree (block_sum)
+  {
     double v[4] = {0.0, 0.0, 0.0, 0.0};
-    if ((unsigned)tid < members) {
+    for (int j = tid; j < (int)members; j += blockDim.x) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = ld_sc1(partials + (grp * kGrp + tid) * 4 + k);
+      for (int k = 0; k < 4; ++k) v[k] += ld_sc1(partials + (grp * kGrp + j) * 4 + k);
     }
+    if (ngr == 1) {  // one group: this workgroup holds the total
+      block_sum<4>(v, red2);
+      if (tid == 0) __hip_atomic_store(&cnt[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ro.sums != nullptr) {
+        double w[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = tid; j < ro.npre; j += blockDim.x) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = wave_sum(v[k]);
+          for (int k = 0; k < 4; ++k) w[k] += ro.pre[(int64_t)j * 4 + k];
+        }
+        block_sum<4>(w, red2);
+        if (tid == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ro.sums[k] = v[k] + w[k];
+        }
+        return;
+      }
+      if (tid == 0) finalize_from(v, ctrl, hist);
+      return;
+    }
+    block_sum<4>(v, red2);
     if (tid == 0) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) st_sc1(gsum + grp * 4 + k, v[k]);
@@ -140,7 +172,6 @@ __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], dou
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] += ld_sc1(gsum + g * 4 + k);
   }
-  __shared__ double red2[4 * 16];
   block_sum<4>(v, red2);
   if (ro.sums != nullptr) {  // reduce-only: + the earlier launch's partials (fixed order)
     double w[4] = {0.0, 0.0, 0.0, 0.0};
