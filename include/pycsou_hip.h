@@ -300,6 +300,14 @@ typedef struct {
   const void* ym;
   const void* zm;
   void* zmn;
+  /* ABI 8: deferred finalization (with hist; NULL = finalize inside the launch).  The launch stores
+   * its partials into `partials` without reducing them and finalizes the PREVIOUS launch's partials,
+   * `fin_partials` (the other of two [nblocks][4] arrays, swapped with the iterate parity -- as
+   * pcs_pds2d_run does), in a workgroup of its own while its tasks run: the reduction leaves the
+   * critical path of every launch.  The stopping rule then acts one launch later (the extra iterate
+   * goes to the buffer the engine does not select: the iterate after Ctrl.it iterations), and the
+   * last launch's partials are finalized by pcs_pds_finalize_pending at the end of a run. */
+  const double* fin_partials;
 } pcs_pds2d_args;
 enum { PCS_M_NONE = 0, PCS_M_L1LOSS = 1 };
 /* 1 if pcs_pds2d_step runs these arguments (0: PCS_EUNSUPPORTED / invalid). */
@@ -468,7 +476,8 @@ int pcs_pds3d_step_bands(const pcs_pds3d_args* a, int64_t a0, int64_t b0, int64_
 
 /* Device control block for the hipGraph-captured loop:
  * int32 [0]=it (next iteration), [1]=stopped, [2]=min_iter, [3]=max_iter, [4]=has_dual,
- * [5]=hist_len; double at byte 32: accuracy_threshold.
+ * [5]=hist_len, [6]=pend (deferred finalization: the last launch's partials wait); double at byte 32:
+ * accuracy_threshold.
  * hist: double[2*(max(min_iter,max_iter)+1)+2] = (primal, dual) relative improvement per iteration. */
 int64_t pcs_ctrl_bytes(void);
 int pcs_ctrl_init(void* ctrl_dev, int min_iter, int max_iter, double thr, int has_dual, hipStream_t stream);
@@ -480,6 +489,11 @@ int pcs_pds_finalize(const double* sums, void* ctrl_dev, double* hist, hipStream
 /* Single-GPU shortcut: pcs_reduce_partials + pcs_pds_finalize in one launch. */
 int pcs_pds_reduce_finalize(const double* partials, int64_t nparts, void* ctrl_dev, double* hist,
                             hipStream_t stream);
+/* End of a deferred-finalization run (pcs_pds2d_args.fin_partials): finalize the last launch's
+ * [nparts][4] partials if they are pending and the loop has not stopped (a no-op otherwise), in the
+ * summation order of the in-launch finalizer. */
+int pcs_pds_finalize_pending(const double* partials, int64_t nparts, void* ctrl_dev, double* hist,
+                             hipStream_t stream);
 /* pcs_ctrl_init with an explicit history length (doubles in `hist`). */
 int pcs_ctrl_init2(void* ctrl_dev, int min_iter, int max_iter, double thr, int has_dual, int hist_len,
                    hipStream_t stream);

@@ -47,7 +47,8 @@ class PdsArgs(ctypes.Structure):
                 ('cty', _vp), ('ntaps', _vp),
                 ('kkind', _c_int), ('edge', _c_int), ('w0', _c_dbl), ('w1', _c_dbl),
                 ('conv_fwd', _vp), ('conv_adj', _vp), ('conv_tier', _c_int), ('pad3', _c_int), ('rbuf', _vp),
-                ('mkind', _c_int), ('pad4', _c_int), ('ym', _vp), ('zm', _vp), ('zmn', _vp)]
+                ('mkind', _c_int), ('pad4', _c_int), ('ym', _vp), ('zm', _vp), ('zmn', _vp),
+                ('fin_partials', _vp)]
 
 
 class StencilArgs(ctypes.Structure):
@@ -168,6 +169,7 @@ _SIGS = {
     'pcs_reduce_partials': (_c_int, [_vp, _c_i64, _vp, _vp]),
     'pcs_pds_finalize': (_c_int, [_vp, _vp, _vp, _vp]),
     'pcs_pds_reduce_finalize': (_c_int, [_vp, _c_i64, _vp, _vp, _vp]),
+    'pcs_pds_finalize_pending': (_c_int, [_vp, _c_i64, _vp, _vp, _vp]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -180,7 +182,7 @@ class HipError(ValueError):
 
 
 # the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 def load():

@@ -21,7 +21,7 @@ __global__ void k_ctrl_init(Ctrl* c, int min_iter, int max_iter, double thr, int
   c->thr = thr;
   c->has_dual = has_dual;
   c->hist_len = hist_len;
-  c->pad0 = c->pad1 = 0;
+  c->pend = c->pad1 = 0;
   const double inf = __builtin_huge_val();
   c->stopped = !((0 <= min_iter) || (0 <= max_iter && inf > thr));
 }
@@ -78,6 +78,13 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_finalize(const double* _
   if (threadIdx.x == 0) finalize_from(v, c, hist);
 }
 
+__global__ __launch_bounds__(kFinLanes) void k_finalize_pending(const double* __restrict__ part, int64_t np, Ctrl* c,
+                                                                double* hist) {
+  __shared__ double red[4 * (kFinLanes / 64)];
+  __shared__ int flag[1];
+  finalize_pending(part, np, c, hist, false, red, flag);
+}
+
 // ---------------------------------------------------------------- host dispatch (planning: pds_host.hpp)
 template <typename T, int FK, int H>
 static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
@@ -88,7 +95,7 @@ static int launch_pds2d(const pcs_pds2d_args* a, hipStream_t st) {
   if (ntiles > 0x7fffffff) return PCS_EUNSUPPORTED;
   const Slab s = make_slab(a);
   const Params<T> P = make_params<T>(a);
-  k_pds2d<T, FK, H, TH, NT><<<(unsigned)ntiles, NT, 0, st>>>(
+  k_pds2d<T, FK, H, TH, NT><<<(unsigned)ntiles + fin_extra(a), NT, 0, st>>>(
       (const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->y, (const T*)a->gbuf, (const T*)a->taps0,
       (const T*)a->taps1, a->half, s, P, a->hkind, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
       tiles_x, (int)ntiles, tiles_x, 0);
@@ -149,7 +156,7 @@ static int launch_pt(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<float> P = make_params<float>(a);
   const float* g = FK == PCS_F_DENOISE ? (const float*)a->y : FK == PCS_F_GRADBUF ? (const float*)a->gbuf : nullptr;
-  k_pds2d_pt<FK, HK><<<(unsigned)p.ntasks, 256, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z,
+  k_pds2d_pt<FK, HK><<<(unsigned)p.ntasks + fin_extra(a), 256, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z,
                                                          (float*)a->zn, g, s, P, a->gkind, a->partials,
                                                          (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x, p.bd,
                                                          p.ntasks);
@@ -279,6 +286,7 @@ int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a) {
 static int check_args(const pcs_pds2d_args* a) {
   if (!a || !a->x || !a->xn || !a->z || !a->zn || !a->partials) return PCS_EINVAL;
   if (a->hist && (!a->ws || !a->ctrl || !aligned16(a->ws) || !aligned16(a->partials))) return PCS_EINVAL;
+  if (a->hist && a->fin_partials == a->partials) return PCS_EINVAL;  // the two arrays of deferred finalization
   if (!a->hist && a->sums_out &&
       (!a->ws || !aligned16(a->ws) || !aligned16(a->partials) || a->n_pre < 0 || a->n_pre > 0x7fffffff ||
        (a->n_pre > 0 && !a->pre_partials)))
@@ -386,9 +394,11 @@ int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t st) {
     if (i % 2) {
       b.x = a->xn, b.xn = const_cast<void*>(a->x), b.z = a->zn, b.zn = const_cast<void*>(a->z);
       b.zm = a->zmn, b.zmn = const_cast<void*>(a->zm);
+      if (a->fin_partials) b.partials = const_cast<double*>(a->fin_partials), b.fin_partials = a->partials;
     } else {
       b.x = a->x, b.xn = a->xn, b.z = a->z, b.zn = a->zn;
       b.zm = a->zm, b.zmn = a->zmn;
+      b.partials = a->partials, b.fin_partials = a->fin_partials;
     }
     const int rc = pcs_pds2d_step(&b, st);
     if (rc != PCS_OK) return rc;
@@ -427,6 +437,12 @@ int pcs_reduce_partials(const double* part, int64_t np, double* sums, hipStream_
 int pcs_pds_finalize(const double* sums, void* ctrl, double* hist, hipStream_t st) {
   if (!sums || !ctrl || !hist) return PCS_EINVAL;
   k_finalize<<<1, 1, 0, st>>>(sums, (Ctrl*)ctrl, hist);
+  return launch_status();
+}
+
+int pcs_pds_finalize_pending(const double* part, int64_t np, void* ctrl, double* hist, hipStream_t st) {
+  if (!part || !ctrl || !hist || np < 1) return PCS_EINVAL;
+  k_finalize_pending<<<1, kFinLanes, 0, st>>>(part, np, (Ctrl*)ctrl, hist);
   return launch_status();
 }
 

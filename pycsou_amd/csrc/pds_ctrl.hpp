@@ -9,7 +9,9 @@
 namespace pcs {
 
 struct Ctrl {
-  int32_t it, stopped, min_iter, max_iter, has_dual, hist_len, pad0, pad1;
+  int32_t it, stopped, min_iter, max_iter, has_dual, hist_len;
+  int32_t pend;  // deferred finalization: the last launch left partials to finalize (fin_slot)
+  int32_t pad1;
   double thr;
   double pad2;
 };
@@ -77,6 +79,7 @@ struct RedOut {
   double* sums;
   const double* pre;
   int npre;
+  const double* fin;  // deferred finalization (single GPU): the previous launch's partials
 };
 
 // Entry test of a step kernel against the sticky stop flag (solver.py:65-66): true = skip the
@@ -103,6 +106,50 @@ __device__ __forceinline__ bool stop_requested(const Ctrl* ctrl, const RedOut& r
   return flag[0] != 0;
 }
 
+// ---- deferred finalization (single GPU, RedOut::fin non-null; pcs_pds2d_args.fin_partials).
+// The step launch of iteration j only stores its workgroups' partials (plain stores, no counters, no
+// waiting on the last arriver); an extra workgroup at the head of the NEXT launch (blockIdx 0 of
+// kFinBlocks leading slots, so that the tasks keep their XCD mapping) sums them in a fixed order and
+// runs finalize_from for iteration j while the tasks of iteration j + 1 run.  When that sets the stop
+// flag the reference loop has ended after iteration j: launch j + 1's iterate (written to the other
+// parity buffer, which held iterate j - 1) is never selected -- the engines read the iterate of
+// parity Ctrl::it -- and its partials are never finalized.  Ctrl::pend says a launch's partials are
+// waiting; pcs_pds_finalize_pending finalizes the last launch's at the end of a run.  The partials
+// alternate between two arrays with the iterate parity.  Summation order: 256 lanes, lane l adds
+// partials l, l + 256, ... in order, then the workgroup tree -- the same in every finalizer.
+constexpr int kFinBlocks = 8;
+constexpr int kFinLanes = 256;
+__device__ __forceinline__ int fin_shift(const RedOut& ro) { return ro.fin != nullptr ? kFinBlocks : 0; }
+
+// `red`: block_sum scratch for the launching kernel's blockDim, `flag`: one int, both LDS
+__device__ __forceinline__ void finalize_pending(const double* __restrict__ prev, int64_t nb, Ctrl* c, double* hist,
+                                                 bool mark, double* red, int* flag) {
+  const int tid = threadIdx.x;
+  if (tid == 0) flag[0] = c->pend && !c->stopped;
+  __syncthreads();
+  if (flag[0]) {  // uniform
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if (tid < kFinLanes) {
+      for (int64_t j = tid; j < nb; j += kFinLanes) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += prev[j * 4 + k];
+      }
+    }
+    block_sum<4>(v, red);  // waves past kFinLanes add exact zeros
+    if (tid == 0) finalize_from(v, c, hist);
+  }
+  if (tid == 0) c->pend = mark ? 1 : 0;
+}
+
+// Kernel entry of a deferring launch: true for the kFinBlocks leading workgroups (the caller returns);
+// workgroup 0 finalizes the previous launch and marks this launch's partials pending.
+__device__ __forceinline__ bool fin_slot(const RedOut& ro, int64_t nblocks, Ctrl* ctrl, double* hist, double* red,
+                                         int* flag) {
+  if (ro.fin == nullptr || blockIdx.x >= kFinBlocks) return false;
+  if (blockIdx.x == 0) finalize_pending(ro.fin, nblocks, ctrl, hist, true, red, flag);
+  return true;
+}
+
 // Called by every thread of every workgroup after thread 0's `part` holds the block sums.
 // `flag` is a 2-int LDS scratch.  With ro.sums the last group writes the sums instead of
 // running finalize_from.
@@ -112,7 +159,7 @@ __device__ __forceinline__ bool stop_requested(const Ctrl* ctrl, const RedOut& r
 #endif
 __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], double* __restrict__ partials,
                                                     int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag,
-                                                    RedOut ro = RedOut{nullptr, nullptr, 0}) {
+                                                    RedOut ro = RedOut{nullptr, nullptr, 0, nullptr}) {
   if (PCS_RED_ABL & 1) return;
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -190,6 +237,20 @@ __device__ __forceinline__ void reduce_and_finalize(const double (&part)[4], dou
   if (tid == 0) {
     __hip_atomic_store(&cnt[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     finalize_from(v, ctrl, hist);
+  }
+}
+
+// The end of a step kernel: publish this workgroup's block sums `part` (thread 0's) -- plain partials
+// of a deferring launch, the in-kernel reduction with hist / ro.sums, else plain partials.
+__device__ __forceinline__ void publish_partials(const double (&part)[4], double* __restrict__ partials,
+                                                 int64_t nblocks, void* ws, Ctrl* ctrl, double* hist, int* flag,
+                                                 RedOut ro) {
+  if (ro.fin == nullptr && (hist != nullptr || ro.sums != nullptr)) {
+    reduce_and_finalize(part, partials, nblocks, ws, ctrl, hist, flag, ro);
+  } else if (threadIdx.x == 0) {
+    const int64_t b = (int64_t)blockIdx.x - fin_shift(ro);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) partials[b * 4 + k] = part[k];
   }
 }
 

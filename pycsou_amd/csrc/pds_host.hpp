@@ -59,7 +59,12 @@ static Params<T> make_params(const pcs_pds2d_args* a) {
 }
 
 static RedOut red_out(const pcs_pds2d_args* a) {
-  return a->hist ? RedOut{nullptr, nullptr, 0} : RedOut{a->sums_out, a->pre_partials, (int)a->n_pre};
+  return a->hist ? RedOut{nullptr, nullptr, 0, a->fin_partials}
+                 : RedOut{a->sums_out, a->pre_partials, (int)a->n_pre, nullptr};
+}
+// workgroups a step launch adds ahead of its tasks (the deferred finalizer slots, pds_ctrl.hpp)
+static unsigned fin_extra(const pcs_pds2d_args* a) {
+  return a->hist && a->fin_partials ? (unsigned)kFinBlocks : 0u;
 }
 
 // ---- fp32 separable conv, tiers 3 and 7: the row-marching kernel (pds_march.hpp) on every

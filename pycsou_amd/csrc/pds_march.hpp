@@ -735,13 +735,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
   __shared__ __attribute__((aligned(16))) T sm[M::SZ];
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntasks, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
   const bool stopped = stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
   int task;
   {
-    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
+    const int b = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
@@ -752,12 +753,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   if (!stopped) march_task<T, H, HK, NT>(x, xn, z, zn, y, taps0, taps1, half, s, P, gk, s0, s1, c0, sm, part);
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {  // the last workgroups reduce (+ finalize)
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  publish_partials(part, partials, ntasks, ws, ctrl, hist, flag, ro);
 }
 
 }  // namespace pcs

@@ -63,21 +63,21 @@ static int launch_march_k(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) 
   if (use_nmarch(a) && a->kkind != PCS_K_GRAD_FORWARD) {
     auto kern = a->kkind == PCS_K_GRAD_BACKWARD ? k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_BACKWARD>
                                                 : k_pds2d_nmarch_gen<float, H, HK, kNMarchNT, PCS_CENTERED>;
-    kern<<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn,
+    kern<<<(unsigned)p.ntasks + fin_extra(a), kNMarchNT, 0, st>>>((const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn,
                                                    (const float*)a->cty, (const float*)a->ntaps, s, P, a->gkind,
                                                    a->edge, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
                                                    p.tiles_x, p.bd, p.ntasks);
     return launch_status();
   }
   if (use_nmarch(a)) {
-    k_pds2d_nmarch<float, H, HK, kNMarchNT><<<(unsigned)p.ntasks, kNMarchNT, 0, st>>>(
+    k_pds2d_nmarch<float, H, HK, kNMarchNT><<<(unsigned)p.ntasks + fin_extra(a), kNMarchNT, 0, st>>>(
         (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->cty,
         (const float*)a->ntaps, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a), p.tiles_x,
         p.bd, p.ntasks);
     return launch_status();
   }
   if (a->kkind != PCS_K_GRAD_FORWARD) return PCS_EUNSUPPORTED;
-  k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks, kMarchNT, 0, st>>>(
+  k_pds2d_march<float, H, HK, kMarchNT><<<(unsigned)p.ntasks + fin_extra(a), kMarchNT, 0, st>>>(
       (const float*)a->x, (float*)a->xn, (const float*)a->z, (float*)a->zn, (const float*)a->y,
       (const float*)a->taps0, (const float*)a->taps1, a->half, s, P, a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist,
       a->ws, red_out(a), p.tiles_x, p.bd, p.ntasks);

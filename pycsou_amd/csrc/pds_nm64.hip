@@ -430,12 +430,13 @@ __global__ __launch_bounds__(512, 1) void k_pds2d_nmarch64(const double* __restr
   double* sm = reinterpret_cast<double*>(nm64_smem);
   __shared__ double red[4 * (M::NT / 64)];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntasks, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
   const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
   const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
   int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
   {
-    const int bb = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
+    const int bb = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
@@ -445,12 +446,7 @@ __global__ __launch_bounds__(512, 1) void k_pds2d_nmarch64(const double* __restr
   if (!stopped) nm64_task<H, HK, KK>(x, xn, z, zn, b, tq, s, P, gk, edge, s0, s1, strip * M::TO, sm, part, stop_raw);
   if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  publish_partials(part, partials, ntasks, ws, ctrl, hist, flag, ro);
 }
 
 // ---------------------------------------------------------------- host side
@@ -520,7 +516,7 @@ static int nm64_go(const pcs_pds2d_args* a, const MarchPlan& p, hipStream_t st) 
   const Slab32 s{(int)s64.n0, (int)s64.n1, (int)s64.row0, (int)s64.rows, s64.hx, s64.hy, s64.hz, s64.vec};
   const Params<double> P = make_params<double>(a);
   nm64_attr<H, HK, KK>();
-  k_pds2d_nmarch64<H, HK, KK><<<(unsigned)p.ntasks, 512, NM64<H>::SZ * sizeof(double), st>>>(
+  k_pds2d_nmarch64<H, HK, KK><<<(unsigned)p.ntasks + fin_extra(a), 512, NM64<H>::SZ * sizeof(double), st>>>(
       (const double*)a->x, (double*)a->xn, (const double*)a->z, (double*)a->zn, (const double*)a->cty,
       (const double*)a->ntaps, s, P, a->gkind, a->edge, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws, red_out(a),
       p.tiles_x, p.bd, p.ntasks);

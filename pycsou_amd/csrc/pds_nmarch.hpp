@@ -1043,13 +1043,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];  // into them never aliases a ring read
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntasks, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
   const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
   const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
   {
-    const int bb = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
+    const int bb = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
@@ -1062,12 +1063,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
     nmarch_task<T, H, HK, NT, PCS_FORWARD>(x, xn, z, zn, b, tq, s, P, gk, 0, s0, s1, c0, sm, zs0, zs1, part, stop_raw);
   if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  publish_partials(part, partials, ntasks, ws, ctrl, hist, flag, ro);
 }
 
 // backward / centred K (KK; `edge` = Gradient(edge=...) of the centred kind): the GEN geometry
@@ -1084,13 +1080,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   __shared__ __attribute__((aligned(16))) T zs1[4 * M::ZSLOTS];
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntasks, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
   const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
   const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
 
   int task;  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips
   {
-    const int bb = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
+    const int bb = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = bb % 8, k = bb / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
@@ -1102,12 +1099,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PCS_NM_WPE))
   if (!stopped) nmarch_task<T, H, HK, NT, KK>(x, xn, z, zn, b, tq, s, P, gk, edge, s0, s1, c0, sm, zs0, zs1, part, stop_raw);
   if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  publish_partials(part, partials, ntasks, ws, ctrl, hist, flag, ro);
 }
 
 }  // namespace pcs

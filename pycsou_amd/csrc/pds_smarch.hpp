@@ -453,12 +453,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   __shared__ __attribute__((aligned(16))) T sm[SMarch<KK>::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntasks, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
   const int stop_raw = stop_flag_early(ctrl, ro);  // consumed in the task (PCS_DEFER_STOP)
   const bool stopped = !stop_deferred(ro) && stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
   int task;
   {  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> adjacent strips of a segment
-    const int b = blockIdx.x, q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
+    const int b = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int seg = task / tiles_x, strip = task - seg * tiles_x;
@@ -476,12 +477,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   }
   if (stop_raw) return;  // the task returned before any store
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {
-    reduce_and_finalize(part, partials, ntasks, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  publish_partials(part, partials, ntasks, ws, ctrl, hist, flag, ro);
 }
 
 }  // namespace pcs

@@ -497,6 +497,7 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   __shared__ __attribute__((aligned(16))) T bufA[SZA];
   __shared__ double red[4 * (NT / 64)];
   __shared__ int flag[2];
+  if (fin_slot(ro, ntiles, ctrl, hist, red, flag)) return;  // deferred finalization (pds_ctrl.hpp)
 
   const bool stopped = stop_requested(ctrl, ro, flag);
   if (stopped && ro.sums == nullptr) return;  // loop already stopped (solver.py:65-66)
@@ -504,7 +505,7 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   // XCD-aware bijective remap: blocks b, b+8, ... share an XCD -> give them adjacent tiles.
   int tile;
   {
-    const int b = blockIdx.x, q = ntiles / 8, r = ntiles % 8, xcd = b % 8, k = b / 8;
+    const int b = (int)blockIdx.x - fin_shift(ro), q = ntiles / 8, r = ntiles % 8, xcd = b % 8, k = b / 8;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   const int ty = tile / tiles_x, txs = tile - ty * tiles_x;
@@ -534,13 +535,8 @@ __global__ __launch_bounds__(NT) void k_pds2d(const T* __restrict__ x, T* __rest
   else
     pds2d_tile<T, FK, H, TH, NT, false>(x, xn, z, zn, y, gbuf, w0, w1, s, P, hk, gk, t0, c0, bufX, bufA, part);
   block_sum<4>(part, red);
-  if (hist != nullptr || ro.sums != nullptr) {
-    // single launch per iteration: last workgroups reduce (+ finalize) in-kernel
-    reduce_and_finalize(part, partials, ntiles, ws, ctrl, hist, flag, ro);
-  } else if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) partials[(int64_t)blockIdx.x * 4 + k] = part[k];
-  }
+  // single launch per iteration: last workgroups reduce (+ finalize) in-kernel, or deferred
+  publish_partials(part, partials, ntiles, ws, ctrl, hist, flag, ro);
 }
 
 }  // namespace pcs

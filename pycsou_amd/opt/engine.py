@@ -39,6 +39,11 @@ NATIVE_MIN_PIXELS = int(os.environ.get('PCS_NATIVE_MIN_PIXELS', 1 << 20))
 
 HIST_CHUNK = 4096  # iterations of device history allocated at first; doubled as the loop goes on
 
+# deferred finalization (pcs_pds2d_args.fin_partials, csrc/pds_ctrl.hpp): each step launch finalizes the
+# previous launch's partials in a workgroup of its own instead of reducing its own at its end.
+# PCS_DEFER_FIN=0: diagnostics, the in-launch reduction.
+DEFER_FIN = os.environ.get('PCS_DEFER_FIN', '1') != '0'
+
 
 def grow_hist(hist, ctrl, need_iters, total):
     """Device history with room for `need_iters` iterations (at most `total`): `hist` itself, or a
@@ -270,8 +275,7 @@ class PDS2DEngine:
         self.fkind = fk
         self.args = a
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
-        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
-        a.partials = self.partials.data_ptr()
+        self._alloc_partials(a, dev)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
         # in-kernel reduce + finalize (one launch per iteration); counters must start at 0
@@ -287,10 +291,31 @@ class PDS2DEngine:
         # replaying a captured graph of the same launches; small images keep the graph
         self.native = fk != L.PCS_F_GRADBUF and self.N >= NATIVE_MIN_PIXELS
 
+    def _alloc_partials(self, a, dev):
+        """[nblocks][4] partials; with deferred finalization two such arrays, swapped with the
+        iterate parity (the launch of parity p writes array p and finalizes array 1 - p)."""
+        self.defer = DEFER_FIN and isinstance(a, L.PdsArgs)
+        nb4 = self.nblocks * 4
+        self.partials = torch.empty((2 if self.defer else 1) * nb4, dtype=torch.float64, device=dev)
+        self.part_halves = [self.partials[:nb4], self.partials[nb4:]] if self.defer else [self.partials]
+        a.partials = self.partials.data_ptr()
+        if self.defer:
+            a.fin_partials = self.part_halves[1].data_ptr()
+
     def _bind(self, a, p):
         """Point the step's iterate buffers at parity p (reads buffers p, writes 1 - p)."""
         a.x, a.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
         a.z, a.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        if getattr(self, 'defer', False):
+            a.partials, a.fin_partials = self.part_halves[p].data_ptr(), self.part_halves[1 - p].data_ptr()
+
+    def _flush(self, next_p, hist):
+        """Deferred finalization: finalize the last launch's partials (parity 1 - next_p) if they
+        are pending (pcs_pds_finalize_pending; a no-op when the loop has stopped)."""
+        if getattr(self, 'defer', False):
+            L.check(self.lib.pcs_pds_finalize_pending(L.ptr(self.part_halves[1 - next_p]), self.nblocks,
+                                                      L.ptr(self.ctrl), L.ptr(hist), L.stream()),
+                    'pcs_pds_finalize_pending')
 
     # the fused step / the chunk of n steps launched back to back from C, on self.args
     def _step_call(self, st):
@@ -373,6 +398,7 @@ class PDS2DEngine:
             a.hist = self.hist.data_ptr()
             self._run_call(int(n))
             self._fixed_p = p ^ (int(n) & 1)
+            self._flush(self._fixed_p, self.hist)
             return
         while n >= self.chunk and p == 0:
             self.graph.replay()
@@ -381,6 +407,7 @@ class PDS2DEngine:
             self._iteration(p, self.hist)
             p ^= 1
         self._fixed_p = p
+        self._flush(p, self.hist)
 
     def time_iteration_kernels(self, n):
         """Median duration (ms) of each kernel of an iteration over n eager iterations, HIP
@@ -420,6 +447,7 @@ class PDS2DEngine:
             self._bind(a, p)
             a.hist = self.hist.data_ptr()
             timed('step', lambda: self._step_call(L.stream()))
+        self._flush(n % 2, self.hist)
         torch.cuda.synchronize()
         return {k: float(np.median([s.elapsed_time(e) for s, e in v])) for k, v in ev.items()}
 
@@ -434,6 +462,7 @@ class PDS2DEngine:
         L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, int(self.hist.numel()), L.stream()),
                 'pcs_ctrl_init2')
         ctrl, hist = a.ctrl, a.hist
+        a.hist = self.hist.data_ptr()
         if not self.fused_finalize:
             a.hist = None
         for i in range(n):
@@ -442,6 +471,7 @@ class PDS2DEngine:
             evs[i][0].record(st)
             self._step_call(L.stream())
             evs[i][1].record(st)
+        self._flush(n % 2, self.hist)
         torch.cuda.synchronize()
         a.ctrl, a.hist = ctrl, hist
         return float(np.mean([s.elapsed_time(e) for s, e in evs]))
@@ -490,6 +520,7 @@ class PDS2DEngine:
                 if int(self.ctrl.view(torch.int32)[1].item()) != 0:
                     break
         hist = self.hist
+        self._flush(0, hist)  # every chunk is an even number of launches
         torch.cuda.synchronize()
         c = self.ctrl.view(torch.int32)[:2].cpu().numpy()
         n = int(c[0])
@@ -598,8 +629,7 @@ class PDS2DStencilEngine(PDS2DEngine):
         nb_fn = self.lib.pcs_pds2d_nblocks if self.march else self.lib.pcs_pds2d_stencil_nblocks
         ws_fn = self.lib.pcs_pds2d_ws_bytes if self.march else self.lib.pcs_pds2d_stencil_ws_bytes
         self.nblocks = int(nb_fn(ctypes.byref(a)))
-        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
-        a.partials = self.partials.data_ptr()
+        self._alloc_partials(a, dev)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
         self.fused_finalize = True
@@ -730,8 +760,7 @@ class PDS2DMaskEngine(PDS2DEngine):
         if self.lib.pcs_pds2d_supported(ctypes.byref(a)) != 1:
             raise ValueError('masked data-fidelity problem not supported by the fused step')
         self.nblocks = int(self.lib.pcs_pds2d_nblocks(ctypes.byref(a)))
-        self.partials = torch.empty(self.nblocks * 4, dtype=torch.float64, device=dev)
-        a.partials = self.partials.data_ptr()
+        self._alloc_partials(a, dev)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
         self.fused_finalize = True

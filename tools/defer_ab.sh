@@ -1,14 +1,14 @@
 #!/bin/bash
-# Library variants on the 2-D legs: C3 headline + c2 / c2_lap / c2_cen / c3_cen, alternating.  $1: out dir, $2..: variants
+# Round 5: deferred finalization A/B (PCS_DEFER_FIN=1, the default, against 0: the in-launch reduction) --
+# the stencil march probe (tools/sm_probe.py) and the 2-D bench legs; $@: the settings to run, in order
 set -o pipefail
-export TMPDIR=/tmp
-out=gpurun_out/$1; shift
+out=gpurun_out/${OUT:-r5_defer}
 mkdir -p $out
-for r in 1 2; do
-  for v in "$@"; do
-    if [ $v = default ]; then L=""; else L=pycsou_amd/lib/var/$v/libpycsou_hip.so; fi
-    PCS_LIB_PATH=$L timeout -k 10 300 python bench.py --steps 400 --warmup 40 --legs c2,c2_lap,c2_cen,c3_cen --volumes "" --no-cpu-baseline 2>/dev/null \
-      | python3 -c "import json,sys; d=json.loads(sys.stdin.read().splitlines()[-1]); print('$v rep $r', 'C3', d['value'], {k: d[k]['it_per_s'] for k in ('c2','c2_lap','c2_cen','c3_cen')})" >> $out/ab.txt || exit 1
-  done
+for v in "$@"; do
+  PCS_DEFER_FIN=$v PCS_N=2048 timeout -k 10 120 python3 tools/sm_probe.py 2>>$out/err.txt | sed "s|^|defer=$v |" | tee -a $out/ab.txt || exit 1
+  PCS_DEFER_FIN=$v timeout -k 10 400 python -u bench.py --steps 300 --warmup 30 --legs ${LEGS:-c2,c2_lap,cps_inpaint,c3_cen,c3_f64} \
+      --volumes "" --no-cpu-baseline > $out/run_$v.json 2>> $out/err.txt || exit 2
+  python -c "
+import json; d=json.load(open('$out/run_$v.json'))
+print('defer=$v', 'C3', d['value'], {k: v.get('it_per_s') for k, v in d.items() if isinstance(v, dict) and 'it_per_s' in v})" | tee -a $out/ab.txt
 done
-cat $out/ab.txt
