@@ -115,10 +115,11 @@ static int pt_slots() {
         nb < 1)
       nb = 4;
     (void)hipGetLastError();
-    // 3 workgroups per CU (fewer, longer row segments) although 5 fit: C2 2048^2 measured
-    // 29.9 us/iteration at 768 workgroups against 35.7 at 1024-2560 and 30.8 at 512
+    // 2 workgroups per CU (fewer, longer row segments) although 5 fit: C2 2048^2 with the deferred
+    // finalization 41.6-43.1 K it/s at 512 workgroups against 40.6-41.2 at 768, 38.7-38.9 at 640, 37.9-38.5 at
+    // 384 and 39.4-39.5 at 1024-1280 (profiles/r5_slots_sweep.txt); 768 with the in-launch reduction
     // (profiles/r1_c2_pt_grid_sweep.txt)
-    slots = cus * (nb < 3 ? nb : 3);
+    slots = cus * (nb < 2 ? nb : 2);
     const char* e = getenv("PCS_PT_SLOTS");  // diagnostics: grid-size sweep
     if (e && atoi(e) > 0) slots = atoi(e);
   }

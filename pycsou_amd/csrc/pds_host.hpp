@@ -161,7 +161,15 @@ static bool sm_forward() {
   return e != nullptr && atoi(e) != 0;
 }
 
-static int sm_slots_for(const pcs_pds2d_args* a) { return a->dtype == PCS_F64 ? sm_slots<double>() : sm_slots<float>(); }
+static int sm_slots_for(const pcs_pds2d_args* a) {
+  if (a->dtype == PCS_F64) return sm_slots<double>();
+  // the masked block (CPS inpainting: z_m and y read, z_m' written on top of the denoising march's words) runs
+  // best at two workgroups per CU: 2048^2 35.9-36.5 K it/s against 34.5 at three, 32.0-32.2 at 2.5 (the other
+  // fp32 K keep three: Laplacian 39.8-40.6 K at two against 41.4-41.5; profiles/r5_slots_sweep.txt)
+  static const bool forced = getenv("PCS_SM_SLOTS") != nullptr;
+  const int s = sm_slots<float>();
+  return a->mkind != PCS_M_NONE && !forced ? s / 3 * 2 : s;
+}
 
 // the fused fp64 normal-operator march (pds_nm64.hip): fp64, separable PSF of tier 3 / 7 with the host's
 // Conv^T y and fp64 N tables, Gradient K of any kind, H = lam L1 / L21; PCS_NM64=0 (read per call): the split
