@@ -108,3 +108,55 @@ def test_c2_fullsize_vs_oracle(kind):
     y = -(s.double().cpu().numpy() if torch.is_tensor(s) else np.asarray(s, np.float64))
     case = {'shape': (n, n), 'y': y, 'meta': dict(meta, niter=NITER)}
     _check(pds, case, torch.float32)
+
+
+def test_cps_fullsize_vs_oracle():
+    """The cps_inpaint bench leg's problem at its size (2048^2, 50 % mask, K = [Masking; Gradient(forward)],
+    H = L1Loss (+) 0.1 L1Norm, G = Segment(0, 1): the masked march, one launch per iteration) against the
+    fp64 oracle's op sequence (pycsou/opt/proxalgs.py:628-716 through the PDS update of :343-394)."""
+    import bench
+    from oracle import pycsou_ref as O
+    from oracle import pylops1 as P
+    from pycsou_amd.func import L1Loss, L1Norm, ProxFuncHStack, Segment
+    from pycsou_amd.linop import Gradient, LinOpVStack, Masking
+    from pycsou_amd.opt import CPS
+    from pycsou_amd.opt.engine import PDS2DMaskEngine
+    n = 2048
+    N = n * n
+    mask = np.random.default_rng(5).random(N) < 0.5
+    m = int(mask.sum())
+    y = bench.phantom((n, n), 12, 5).ravel()[mask].astype(np.float32)
+    Kop = LinOpVStack(Masking(size=N, sampling_bool=mask), Gradient(shape=(n, n), kind='forward'))
+    Kop.lipschitz_cst = Kop.diff_lipschitz_cst = 3.0
+    cps = CPS(dim=N, G=Segment(dim=N, a=0, b=1), H=ProxFuncHStack(L1Loss(dim=m, data=y), 0.1 * L1Norm(dim=2 * N)),
+              K=Kop, x0=np.zeros(N, np.float32), z0=np.zeros(m + 2 * N, np.float32), max_iter=NITER - 1,
+              min_iter=NITER - 1, accuracy_threshold=0.0, verbose=None)
+    est, _, diag = cps.iterate()
+    assert isinstance(cps._engine, PDS2DMaskEngine) and cps.iter == NITER
+    D = P.Gradient((n, n), sampling=1., edge=True, kind='forward')
+    yd = y.astype(np.float64)
+
+    def Kf(x):
+        return np.concatenate([x[mask], D.matvec(x)])
+
+    def KT(z):
+        xa = np.zeros(N)
+        xa[mask] = z[:m]
+        return 0 + xa + D.rmatvec(z[m:])
+
+    hs = O.postcomp(O.prox_l1, 0.1)
+
+    def hprox(v, t):
+        return np.concatenate([O.prox_l1(v[:m] + (-yd), t) - (-yd), hs(v[m:], t)])
+
+    xr, zr, dr = O.pds(lambda x: np.zeros_like(x), lambda v, t: O.proj_segment(v, 0.0, 1.0), Kf, KT,
+                       lambda w, s: O.fenchel_prox(hprox, w, s), cps.tau, cps.sigma, cps.rho, np.zeros(N),
+                       np.zeros(m + 2 * N), max_iter=NITER - 1, min_iter=NITER - 1, accuracy_threshold=0.0)
+    x = np.asarray(est['primal_variable'], np.float64)
+    z = np.asarray(est['dual_variable'], np.float64)
+    assert rel(x, xr) < 5e-5, rel(x, xr)
+    assert rel(z, zr) < 5e-5, rel(z, zr)
+    np.testing.assert_allclose(diag['Relative Improvement (primal variable)'].to_numpy(float)[1:],
+                               np.asarray(dr['primal'])[1:], rtol=1e-3)
+    np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float)[1:],
+                               np.asarray(dr['dual'])[1:], rtol=1e-3)
