@@ -595,6 +595,7 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
   const int ze = min(tid, NZ - 1), zi = ze / (TW / 4), zg = ze - zi * (TW / 4);
   const int i1z = r1 + zi, c_z = c2 + 4 * zg;
   // the tile's u region (rows r1-1 .. r1+T1, cols c2-4 .. c2+TW+3) >= 2 samples inside the plane
+  // the tile's u region (rows r1-1 .. r1+T1, cols c2-4 .. c2+TW+3) >= 2 samples inside the plane
   const bool tile_int = r1 - 1 >= 2 && r1 + T1 <= v.n1 - 3 && c2 - 4 >= 2 && c2 + TW + 3 <= v.n2 - 3;
 
   // loads run two planes ahead: iteration p lands set p & 1 and refills it with plane p + 2's data
@@ -665,8 +666,8 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
       lds_barrier();
       // ---- U items: x_t, u on the u region of plane p; x' on own voxels (I: every sample of the
       // tile's u region and plane p lies >= 2 samples inside the volume -- no edge rules)
-      auto u_items = [&](auto intc) {
-        constexpr bool I = decltype(intc)::value;
+      auto u_items = [&](auto ic0, auto ic12, auto ic2) {  // interior along axis 0 / axis 1 / axis 2
+        constexpr bool I0 = decltype(ic0)::value, I1 = decltype(ic12)::value, I2 = decltype(ic2)::value;
 #pragma unroll
         for (int k = 0; k < KU; ++k) {
           if (k * NT + tid >= NU) continue;
@@ -691,9 +692,9 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
             const T w1[5] = {T(0), y0.v[m], y1.v[m], y2.v[m], T(0)};
             const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
             // K^T z, VStack order ((D0^T z0 + D1^T z1) + D2^T z2), each sum scaled by 1/h once
-            const T kt = pcs_fma(sw_d1_adj<KK, I>(w2, i2, v.n2, edge), P.inv_step[2],
-                                 pcs_fma(sw_d1_adj<KK, I>(w1, i1, v.n1, edge), P.inv_step[1],
-                                         sw_d1_adj<KK, I>(w0, gp, v.n0, edge) * P.inv_step[0]));
+            const T kt = pcs_fma(sw_d1_adj<KK, I2>(w2, i2, v.n2, edge), P.inv_step[2],
+                                 pcs_fma(sw_d1_adj<KK, I1>(w1, i1, v.n1, edge), P.inv_step[1],
+                                         sw_d1_adj<KK, I0>(w0, gp, v.n0, edge) * P.inv_step[0]));
             const T xv = xv4[k].v[m];
             T gf;
             if constexpr (FK == PCS_F_NULL) gf = T(0);
@@ -715,12 +716,20 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
           st4(&U[s0][o], uo);
         }
       };
-      if (tile_int && gp >= 2 && gp <= v.n0 - 3) u_items(std::true_type{});
-      else u_items(std::false_type{});
+      // three forms: interior; the edge rules on the row and column axes only (the tiles along the plane's
+      // border, on every plane but the first / last two); the edge rules on every axis.  With one task per
+      // CU the kernel ends with its slowest task: the border row tiles on the all-axes form held C4 centred
+      // at 1.37-1.42 ms against 1.11 with every tile interior (profiles/r5_g3d_edge_ab.txt)
+      using Tt = std::true_type;
+      using Ff = std::false_type;
+      const bool pint_u = gp >= 2 && gp <= v.n0 - 3;
+      if (tile_int && pint_u) u_items(Tt{}, Tt{}, Tt{});
+      else if (pint_u) u_items(Tt{}, Ff{}, Ff{});
+      else u_items(Ff{}, Ff{}, Ff{});
       lds_barrier();
       // ---- z' items for plane q = p - 1 (own tile)
-      auto z_items = [&](auto intc) {
-        constexpr bool I = decltype(intc)::value;
+      auto z_items = [&](auto ic0, auto ic12, auto ic2) {
+        constexpr bool I0 = decltype(ic0)::value, I1 = decltype(ic12)::value, I2 = decltype(ic2)::value;
         if (p > p_start && tid < NZ) {
           const int q = p - 1, gq = gp - 1;
           const int o = (zi + 1) * WU + 4 * (zg + 1);
@@ -741,9 +750,9 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
             const T w0[5] = {T(0), ua.v[m], ub.v[m], uc.v[m], T(0)};
             const T w1[5] = {T(0), un.v[m], ub.v[m], us.v[m], T(0)};
             const T w2[5] = {T(0), h2[m], h2[m + 1], h2[m + 2], T(0)};
-            const T k0 = sw_d1_fwd<KK, I>(w0, gq, v.n0, P.inv_step[0], edge);
-            const T k1 = sw_d1_fwd<KK, I>(w1, i1z, v.n1, P.inv_step[1], edge);
-            const T k2 = sw_d1_fwd<KK, I>(w2, i2, v.n2, P.inv_step[2], edge);
+            const T k0 = sw_d1_fwd<KK, I0>(w0, gq, v.n0, P.inv_step[0], edge);
+            const T k1 = sw_d1_fwd<KK, I1>(w1, i1z, v.n1, P.inv_step[1], edge);
+            const T k2 = sw_d1_fwd<KK, I2>(w2, i2, v.n2, P.inv_step[2], edge);
             const T w0v = zv0.v[m] + P.sigma * k0, w1v = zv1.v[m] + P.sigma * k1, w2v = zv2.v[m] + P.sigma * k2;
             const T v0 = w0v * P.inv_sigma, v1 = w1v * P.inv_sigma, v2 = w2v * P.inv_sigma;
             T t0, t1, t2;
@@ -775,8 +784,10 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
           }
         }
       };
-      if (tile_int && gp - 1 >= 2 && gp - 1 <= v.n0 - 3) z_items(std::true_type{});
-      else z_items(std::false_type{});
+      const bool pint_z = gp - 1 >= 2 && gp - 1 <= v.n0 - 3;
+      if (tile_int && pint_z) z_items(Tt{}, Tt{}, Tt{});
+      else if (pint_z) z_items(Tt{}, Ff{}, Ff{});
+      else z_items(Ff{}, Ff{}, Ff{});
   };
   for (int p = p_start - 1; p <= p_end; p += 2) {
     iter(p, S0{});

@@ -114,11 +114,16 @@ __device__ __forceinline__ T sw_d1_adj(const T (&w)[5], int i, int n, int edge) 
     const T t3 = (INT || i <= n - 3) ? w[3] : T(0);
     const T t1 = (INT || i >= 2) ? w[1] : T(0);
     T acc = T(0.5) * (t1 - t3);
-    if (!INT && edge && n >= 2) {  // only rows within 2 of an edge, which INT never covers
-      if (i == 0) acc -= w[2];
-      if (i == 1) acc += w[1];
-      if (i == n - 2) acc -= w[3];
-      if (i == n - 1) acc += w[2];
+    if constexpr (!INT) {  // only rows within 2 of an edge, which INT never covers
+      // selects in the rules' order (n = 2, 3 apply several), the uniform edge test folded into each:
+      // an `if (edge ...)` here is a scalar branch per sample and axis, which splits the plane march's
+      // unrolled item loops into basic blocks of ~8 instructions (k_pds3d_gen's border tiles ran 1.5x
+      // their interior time, profiles/r5_g3d_edge_ab.txt)
+      const bool e = edge && n >= 2;
+      acc = (e && i == 0) ? acc - w[2] : acc;
+      acc = (e && i == 1) ? acc + w[1] : acc;
+      acc = (e && i == n - 2) ? acc - w[3] : acc;
+      acc = (e && i == n - 1) ? acc + w[2] : acc;
     }
     return acc;
   }
@@ -136,13 +141,14 @@ __device__ __forceinline__ T sw_d2_adj(const T (&w)[5], int i, int n, int edge) 
   const T t2 = (INT || (i >= 1 && i <= n - 2)) ? w[2] : T(0);
   const T t1 = (INT || i >= 2) ? w[1] : T(0);
   T acc = (t3 - T(2) * t2) + t1;
-  if (!INT && edge && n >= 3) {
-    if (i == 0) acc += w[2];
-    if (i == 1) acc -= T(2) * w[1];
-    if (i == 2) acc += w[0];
-    if (i == n - 3) acc += w[4];
-    if (i == n - 2) acc -= T(2) * w[3];
-    if (i == n - 1) acc += w[2];
+  if constexpr (!INT) {  // selects in the rules' order, the edge test folded in (sw_d1_adj)
+    const bool e = edge && n >= 3;
+    acc = (e && i == 0) ? acc + w[2] : acc;
+    acc = (e && i == 1) ? acc - T(2) * w[1] : acc;
+    acc = (e && i == 2) ? acc + w[0] : acc;
+    acc = (e && i == n - 3) ? acc + w[4] : acc;
+    acc = (e && i == n - 2) ? acc - T(2) * w[3] : acc;
+    acc = (e && i == n - 1) ? acc + w[2] : acc;
   }
   return acc;
 }
