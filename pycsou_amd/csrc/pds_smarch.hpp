@@ -468,7 +468,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
-    if (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1)  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
+#ifndef PCS_SM_ALLCI  // diagnostics (timing only, wrong border columns): every strip on the interior form
+#define PCS_SM_ALLCI 0
+#endif
+    if (PCS_SM_ALLCI || (c0 >= 4 && c0 + SMarch<KK>::TW + 6 <= s.n1))  // columns [c0 - 2, c0 + 66) >= 2 inside: no column edge rule
       smarch_task<T, KK, FK, HK, true>(x, xn, z, zn, gsrc, bsrc, msrc, mdst, s, P, Q, gk, s0, s1, c0, sm, part,
                                            stop_raw);
     else
