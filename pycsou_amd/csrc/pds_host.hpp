@@ -76,6 +76,7 @@ struct MarchPlan {
   int tiles_x;  // 64-column strips
   Bands bd;     // row segments of the launch's bands
   int ntasks;   // strips x segments
+  StripSplit sp{-1, 0, 0, 0, {0, 0, 0}, Bands{16, 0, 0, 0, 0, 0}};  // border strips on shorter segments (sm_plan)
 };
 
 // own-row bands [ra0, rb0) and [ra1, rb1) of a launch (0 <= ra0 <= rb0 <= ra1 <= rb1 <= rows)
@@ -202,7 +203,46 @@ static bool sm_plan(const pcs_pds2d_args* a, RowBands rb, MarchPlan* p) {
   const int tiles_x = (int)((a->n1 + 63) / 64);
   if (tiles_x < 2) return false;
   // segments of at least 4 16-row steps (fp64: 8)
-  plan_bands(rb, 16, tiles_x, sm_slots_for(a), a->dtype == PCS_F64 ? 8 : 4, p);
+  const int slots = sm_slots_for(a);
+  plan_bands(rb, 16, tiles_x, slots, a->dtype == PCS_F64 ? 8 : 4, p);
+  // fp32, one band, backward / centred K or the Laplacian: the border strips (the first, and the last ones
+  // whose 4-column margin reaches past n1 - 3) run the column edge rules on every element, so in the one-round
+  // grid their tasks end the launch -- 2048^2 Laplacian 23.9 us against 19.3 with interior arithmetic
+  // everywhere (profiles/r5_sm_allci_ab.txt).  They get shorter segments (a step count scaled by r), within
+  // the same slots.  PCS_SM_SPLIT=0 (read once): one segmentation for every strip
+  static const int split_on = [] {
+    const char* e = getenv("PCS_SM_SPLIT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const bool one_band = rb.rb0 == rb.ra0 || rb.rb1 == rb.ra1;
+  if (!split_on || a->dtype != PCS_F32 || !one_band || tiles_x < 4 || a->kkind == PCS_K_GRAD_FORWARD) return true;
+  const double r = a->kkind == PCS_K_LAPLACIAN ? 0.8 : 0.85;  // border / interior task steps
+  if (rb.rb0 == rb.ra0) rb = RowBands{rb.ra1, rb.rb1, rb.rb1, rb.rb1};
+  const int64_t L = rb.rb0 - rb.ra0, steps = (L + 15) / 16;
+  int nright = 0;
+  for (int j = tiles_x - 1; j >= 1 && 64 * j + 70 > a->n1; --j) ++nright;
+  const int nbs = 1 + nright, iw = tiles_x - nbs;
+  if (nbs > 3 || iw < 1) return true;
+  // only where the split keeps the interior segments as they were (4096^2: it would lengthen them 22 -> 24
+  // steps and measured 0.5-1 % slower; 2048^2 keeps 6: Laplacian 23.7 -> 20.0 us, centred 25.3 -> 24.6)
+  const int64_t li0 = p->bd.seg_len / 16;
+  for (int64_t li = 4; li <= li0; ++li) {
+    const int64_t lb = (int64_t)(li * r);
+    if (lb < 2 || lb >= li) continue;
+    const int64_t ni = (steps + li - 1) / li, nb = (steps + lb - 1) / lb;
+    if (iw * ni + nbs * nb > slots) continue;
+    p->bd = Bands{(int)(16 * li), (int)((L + 16 * li - 1) / (16 * li)), (int)rb.ra0, (int)rb.rb0, (int)rb.rb0, (int)rb.rb0};
+    p->sp.bdb = Bands{(int)(16 * lb), (int)((L + 16 * lb - 1) / (16 * lb)), (int)rb.ra0, (int)rb.rb0, (int)rb.rb0,
+                      (int)rb.rb0};
+    p->sp.nint = iw * p->bd.nseg0;
+    p->sp.ilo = 1;
+    p->sp.iw = iw;
+    p->sp.nbs = nbs;
+    p->sp.bs[0] = 0;
+    for (int k = 1; k < nbs; ++k) p->sp.bs[k] = tiles_x - k;
+    p->ntasks = p->sp.nint + nbs * p->sp.bdb.nseg0;
+    return true;
+  }
   return true;
 }
 

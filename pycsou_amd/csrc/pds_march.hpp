@@ -89,6 +89,14 @@ __device__ __forceinline__ unsigned long long pcs_stamp() {
 struct Bands {
   int seg_len, nseg0, ra0, rb0, ra1, rb1;
 };
+// Border-strip split of a row-march launch (the stencil march): tasks [0, nint) run the interior strips
+// [ilo, ilo + iw) with segments bd, tasks [nint, ntasks) the border strips bs[0 .. nbs) with the shorter
+// segments bdb.  nint < 0: one segmentation for every strip (task = seg * tiles_x + strip).
+struct StripSplit {
+  int nint, ilo, iw, nbs;
+  int bs[3];
+  Bands bdb;
+};
 __device__ __forceinline__ void band_rows(const Bands& bd, int seg, int& s0, int& s1) {
   if (seg < bd.nseg0) {
     s0 = bd.ra0 + seg * bd.seg_len;

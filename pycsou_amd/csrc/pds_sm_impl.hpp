@@ -60,7 +60,7 @@ static int launch_smarch(const pcs_pds2d_args* a, RowBands rb, hipStream_t st) {
   T* mo = FK == SM_F_MASK ? (T*)a->zmn : nullptr;
   k_pds2d_smarch<T, KK, FK, HK><<<(unsigned)p.ntasks + fin_extra(a), 256, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, g, b, mi, mo, s, P,
                                            make_sparams<T>(a), a->gkind, a->partials, (Ctrl*)a->ctrl, a->hist, a->ws,
-                                           red_out(a), p.tiles_x, p.bd, p.ntasks);
+                                           red_out(a), p.tiles_x, p.bd, p.ntasks, p.sp);
   return launch_status();
 }
 

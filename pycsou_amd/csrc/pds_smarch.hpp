@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
                                                        T* __restrict__ mdst, Slab32 s, Params<T> P,
                                                        SParamsT<T> Q, int gk, double* __restrict__ partials, Ctrl* ctrl,
                                                        double* hist, void* ws, RedOut ro, int tiles_x, Bands bd,
-                                                       int ntasks) {
+                                                       int ntasks, StripSplit sp) {
   __shared__ __attribute__((aligned(16))) T sm[SMarch<KK>::SZ];
   __shared__ double red[4 * 4];
   __shared__ int flag[2];
@@ -462,9 +462,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCS_SM_WPE)
     const int b = (int)blockIdx.x - fin_shift(ro), q = ntasks / 8, r = ntasks % 8, xcd = b % 8, k = b / 8;
     task = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
-  const int seg = task / tiles_x, strip = task - seg * tiles_x;
-  int s0, s1;
-  band_rows(bd, seg, s0, s1);
+  int strip, s0, s1;
+  if (sp.nint < 0) {  // one segmentation for every strip
+    const int seg = task / tiles_x;
+    strip = task - seg * tiles_x;
+    band_rows(bd, seg, s0, s1);
+  } else if (task < sp.nint) {  // interior strips
+    const int seg = task / sp.iw;
+    strip = sp.ilo + task - seg * sp.iw;
+    band_rows(bd, seg, s0, s1);
+  } else {  // border strips, shorter segments
+    const int b = task - sp.nint, seg = b / sp.nbs, j = b - seg * sp.nbs;
+    strip = j == 0 ? sp.bs[0] : (j == 1 ? sp.bs[1] : sp.bs[2]);
+    band_rows(sp.bdb, seg, s0, s1);
+  }
   double part[4] = {0.0, 0.0, 0.0, 0.0};
   const int c0 = strip * SMarch<KK>::TW;
   if (!stopped) {
