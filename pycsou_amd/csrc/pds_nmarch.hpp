@@ -41,11 +41,6 @@
 #ifndef PCS_NM_EDGE
 #define PCS_NM_EDGE 1
 #endif
-// b (= Conv^T y) rows loaded a whole step ahead of their use (1) or at the top of the step that uses
-// them (0: only PH hides their latency)
-#ifndef PCS_NM_BAHEAD
-#define PCS_NM_BAHEAD 0
-#endif
 // cache-policy bits of the x' / z' stores (16 = sc1: written through, not left dirty in L2)
 // C2 2048^2: 31.4 against 32.3 us per iteration, C3 4096^2: 112.7 against 113.9 us (two alternating
 // reps each, profiles/r3_store_policy_ab.txt)
@@ -890,7 +885,6 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     part[3] += (double)sz;
   };
   constexpr bool COLS = !GEN && PCS_NM_COLS;
-  static_assert(!COLS || !PCS_NM_BAHEAD, "the column layout loads b at the top of its step");
   // b of the column layout: rows r0 + 4 wv + o, column cc
   auto load_bc = [&](T (&bc)[4], int r0) {
 #pragma unroll
@@ -968,16 +962,6 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 
   // ================= march: step k covers t rows [a+2H+1, a+2H+17), u / x' rows [a+1, a+17), z' rows [a, a+16)
   const int nsteps = (s1 - s0 + TS - 1) / TS;
-#if PCS_NM_BAHEAD
-  G4<T> bvn;  // b of the next step's update rows
-  T b5n, bm1n = T(0);
-  {
-    const uint32_t rb = vb.row_off(s0 + 1 + ui);
-    bvn = bload4(vb.r, rb + co_u);
-    b5n = load_b5(s0 + 1);
-    if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(s0 + 1 + eur) + co_bx), 0, 0));
-  }
-#endif
   int ub = 0;  // (16 k) mod UR: row r = a + j sits in u ring slot (j + ub) mod UR
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
@@ -988,33 +972,36 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
 #if PCS_NM_PRIO
     __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
 #endif
-    load_z(a, 0);
-#if PCS_NM_BAHEAD
-    bv = bvn;
-    b5 = b5n;
-    bm1 = bm1n;
-    {
-      const uint32_t rb = vb.row_off(a + 1 + TS + ui);
-      bvn = bload4(vb.r, rb + co_u);
-      b5n = load_b5(a + 1 + TS);
-      if constexpr (GEN) bm1n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + TS + eur) + co_bx), 0, 0));
-    }
-#else
-    if constexpr (COLS) {
-      load_bc(bc, a + 1);
+    // The z tiles land through LDS-DMA loads; before the barrier that precedes their first read the wave
+    // waits until only the loads it issued after them are outstanding.  Forward K: b (bv, b5) and the x
+    // rows, counted.  GEN: its b values (bm1 of the extra-column lanes, b5 of the last group) are used on
+    // subsets of lanes only, and the compiler sinks those loads to their uses past the wait -- counted,
+    // they left the last tile load in flight when the tiles were read (a race: the C3 centred iterate
+    // differed between runs from the second iteration on).  GEN therefore issues every load ahead of the
+    // tiles and waits for all of them (tools/vmcnt_check.py checks the counts in the assembly).
+    if constexpr (GEN) {
+      bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
+      bv = bload4a<PCS_NM_LAUX>(vb.r, vb.row_off(a + 1 + ui) + co_u);
+      b5 = load_b5(a + 1);
+      load_xn(xnx, a + 2 * H + 1 + TS);
+      load_z(a, 0);
     } else {
-      const uint32_t rb = vb.row_off(a + 1 + ui);
-      bv = bload4a<PCS_NM_LAUX>(vb.r, rb + co_u);
+      load_z(a, 0);
+      if constexpr (COLS) {
+        load_bc(bc, a + 1);
+      } else {
+        const uint32_t rb = vb.row_off(a + 1 + ui);
+        bv = bload4a<PCS_NM_LAUX>(vb.r, rb + co_u);
+      }
+      b5 = load_b5(a + 1);
+      load_xn(xnx, a + 2 * H + 1 + TS);
     }
-    b5 = load_b5(a + 1);
-    if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
-#endif
-    load_xn(xnx, a + 2 * H + 1 + TS);
 #if PCS_NM_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
     ph(a + 2 * H + 1 + ui);
-    vm_wait<KXN + (COLS ? 5 : 2 + PR)>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
+    if constexpr (GEN) vm_wait<0>();
+    else vm_wait<KXN + (COLS ? 5 : 2)>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
     if constexpr (COLS) pvc(a, bc, b5, ub);
     else pv(a, bv, b5, bm1, ub);

@@ -329,3 +329,31 @@ def test_pds2d_masked_block_and_fp64_dispatch():
     a.gbuf = 0x20000
     assert lib.pcs_pds2d_supported(ctypes.byref(a)) == 1
     assert lib.pcs_pds2d_nblocks(ctypes.byref(a)) != nb_tile  # the march's task count
+
+
+def test_lds_dma_waits_cover_the_tiles(tmp_path):
+    """The row marches land their z tiles with LDS-DMA loads and wait, before the barrier that precedes the
+    tiles' first read, until only the loads issued after them are outstanding.  A load the compiler sinks
+    past that wait breaks the count (round 5: the centred normal-operator march read a tile still in
+    flight, and its iterate differed between runs).  Compile the two march units to gfx950 assembly and
+    check every march kernel's loop: the wait's count never exceeds the loads issued after the last tile
+    load (tools/vmcnt_check.py)."""
+    import shutil
+    import subprocess
+    import sys
+    hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
+    if not os.path.exists(hipcc):
+        pytest.skip('hipcc not available')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for unit in ('pds_nm', 'pds_nm64'):
+        out = str(tmp_path / f'{unit}.s')
+        subprocess.run([hipcc, '--offload-arch=gfx950', '-O3', '-fno-slp-vectorize', '-std=c++17',
+                        '-I' + os.path.join(root, 'include'), '--cuda-device-only', '-S',
+                        os.path.join(root, 'pycsou_amd', 'csrc', unit + '.hip'), '-o', out],
+                       check=True, capture_output=True, timeout=600)
+        outs.append(out)
+    r = subprocess.run([sys.executable, os.path.join(root, 'tools', 'vmcnt_check.py')] + outs, capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count('ok ') >= 12, r.stdout
