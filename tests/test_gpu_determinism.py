@@ -42,3 +42,20 @@ def test_fused_march_is_deterministic(name):
         assert torch.equal(x, runs[0][1]), int((x != runs[0][1]).sum())
         assert torch.equal(z, runs[0][2]), int((z != runs[0][2]).sum())
         assert np.array_equal(h, runs[0][3])
+
+
+@pytest.mark.parametrize('kind', ['forward', 'centered'])
+def test_fused_3d_step_is_deterministic(kind):
+    """The 3-D engine (k_pds3d with the folded axis-0 pass / k_pds3d_gen + the in-plane normal operator)
+    through the public API, three runs of 8 iterations at 96^3: bitwise the same iterate and dual."""
+    import bench
+    outs = []
+    for _ in range(3):
+        pds = bench.build_volume(96, torch.float32, kind=kind)
+        pds.max_iter, pds.min_iter, pds.accuracy_threshold = 7, 7, 0.0
+        est, _, diag = pds.iterate()
+        assert pds._engine is not None and pds.iter == 8
+        outs.append((est['primal_variable'].clone(), est['dual_variable'].clone()))
+    for x, z in outs[1:]:
+        assert torch.equal(x, outs[0][0]), int((x != outs[0][0]).sum())
+        assert torch.equal(z, outs[0][1]), int((z != outs[0][1]).sum())
