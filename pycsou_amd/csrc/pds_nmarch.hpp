@@ -979,8 +979,12 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     // they left the last tile load in flight when the tiles were read (a race: the C3 centred iterate
     // differed between runs from the second iteration on).  GEN therefore issues every load ahead of the
     // tiles and waits for all of them (tools/vmcnt_check.py checks the counts in the assembly).
-    if constexpr (GEN) {
-      bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
+#ifndef PCS_NM_LOADFIRST  // diagnostics: the forward kernel with GEN's load order and full wait
+#define PCS_NM_LOADFIRST 0
+#endif
+    constexpr bool LF = GEN || (PCS_NM_LOADFIRST && !COLS);
+    if constexpr (LF) {
+      if constexpr (GEN) bm1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vb.r, (int)(vb.row_off(a + 1 + eur) + co_bx), 0, 0));
       bv = bload4a<PCS_NM_LAUX>(vb.r, vb.row_off(a + 1 + ui) + co_u);
       b5 = load_b5(a + 1);
       load_xn(xnx, a + 2 * H + 1 + TS);
@@ -1000,7 +1004,7 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     __builtin_amdgcn_s_setprio(0);
 #endif
     ph(a + 2 * H + 1 + ui);
-    if constexpr (GEN) vm_wait<0>();
+    if constexpr (LF) vm_wait<0>();
     else vm_wait<KXN + (COLS ? 5 : 2)>();  // this wave's z tile loads have landed (b and the x rows may be in flight)
     lds_barrier();
     if constexpr (COLS) pvc(a, bc, b5, ub);
