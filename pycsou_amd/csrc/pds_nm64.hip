@@ -390,11 +390,14 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
   }
   // ================= march
   const int nsteps = (s1 - s0 + TS - 1) / TS;
-  const bool cint = cb >= 2 && cb + M::CW + 2 <= n1;  // the strip's columns [cb, cb + 64) >= 2 inside
+#ifndef PCS_NM64_ALLINT  // diagnostics (timing only, wrong border values): every strip and step on the interior form
+#define PCS_NM64_ALLINT 0
+#endif
+  const bool cint = PCS_NM64_ALLINT || (cb >= 2 && cb + M::CW + 2 <= n1);  // the strip's columns [cb, cb + 64) >= 2 inside
   for (int k = 0; k < nsteps; ++k) {
     const int a = s0 + k * TS;
     // U rows [a + 1, a + 33) and Z rows [a, a + 32) >= 2 inside the image (uniform)
-    const bool rint = cint && s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0;
+    const bool rint = PCS_NM64_ALLINT || (cint && s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0);
     lds_barrier();  // step k - 1 done with the z tiles and the u ring; this step's x rows have landed
     __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
     load_z(a, 0);
