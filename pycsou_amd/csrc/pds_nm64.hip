@@ -394,10 +394,8 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
 #define PCS_NM64_ALLINT 0
 #endif
   const bool cint = PCS_NM64_ALLINT || (cb >= 2 && cb + M::CW + 2 <= n1);  // the strip's columns [cb, cb + 64) >= 2 inside
-  for (int k = 0; k < nsteps; ++k) {
-    const int a = s0 + k * TS;
-    // U rows [a + 1, a + 33) and Z rows [a, a + 32) >= 2 inside the image (uniform)
-    const bool rint = PCS_NM64_ALLINT || (cint && s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0);
+  // one step; RI: its U rows [a + 1, a + 33) and Z rows [a, a + 32) >= 2 inside the image
+  auto step = [&](int a, auto ri) {
     lds_barrier();  // step k - 1 done with the z tiles and the u ring; this step's x rows have landed
     __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
     load_z(a, 0);
@@ -407,15 +405,30 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
     ph(a + 2 * H + 1 + pr);
     __builtin_amdgcn_s_waitcnt((NXL & 15) | ((NXL >> 4) << 14) | (7 << 4) | (15 << 8));  // z tiles and b landed
     lds_barrier();
-    if (rint) pvu(std::true_type{}, a, bv, a);
-    else pvu(std::false_type{}, a, bv, a);
+    pvu(ri, a, bv, a);
     lds_barrier();
-    if (rint) zph(std::true_type{}, a);
-    else zph(std::false_type{}, a);
+    zph(ri, a);
     // the next step's x rows (in flight behind: 2 x' and 4 z' stores) into the slots of rows [a + 2H - 15,
     // a + 2H + 17), which this step's PH and U were the last to read
     __builtin_amdgcn_s_waitcnt((6 & 15) | (7 << 4) | (15 << 8));
     store_x(xnx, a + TS + 2 * H + 1, TS);
+  };
+  auto rint_of = [&](int a) {
+    return PCS_NM64_ALLINT || (cint && s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0);
+  };
+#ifndef PCS_NM64_PEEL  // diagnostics: 0 = one loop choosing the form per step
+#define PCS_NM64_PEEL 1
+#endif
+  if (PCS_NM64_PEEL && rint_of(s0) && rint_of(s0 + (nsteps - 1) * TS)) {
+    // every step of the task interior (uniform): a loop holding the interior form only -- with both
+    // forms in the loop body the interior steps ran slower (profiles/r5_nm64_split_ab.txt)
+    for (int k = 0; k < nsteps; ++k) step(s0 + k * TS, std::true_type{});
+  } else {
+    for (int k = 0; k < nsteps; ++k) {
+      const int a = s0 + k * TS;
+      if (rint_of(a)) step(a, std::true_type{});
+      else step(a, std::false_type{});
+    }
   }
 }
 
