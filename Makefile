@@ -13,10 +13,6 @@ build/%.o: pycsou_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) $(FLAGS_$*) -c $< -o $@
 
-# corr2d.hip: MFMA accumulators in VGPRs (gfx950's unified file) -- k_corr2d_mf rewrites one accumulator
-# register per input row, which in AGPRs costs a read + write of the whole 4-register tuple
-FLAGS_corr2d := -mllvm -amdgpu-mfma-vgpr-form
-
 $(LIB): $(OBJ)
 	@mkdir -p pycsou_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ) -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib

@@ -330,6 +330,8 @@ int pcs_pds2d_ntaps_len(int half); /* 64 + 32 * tier(half); -1 beyond tier 7 */
 int pcs_pds2d_halo_x(int half);
 int64_t pcs_pds2d_nblocks(const pcs_pds2d_args* a);
 int64_t pcs_pds2d_ws_bytes(const pcs_pds2d_args* a);
+/* One iteration (x, z -> xn, zn).  With fin_partials the launch finalizes the previous launch's
+ * partials, not its own: see pcs_pds2d_run for the stop semantics and pcs_pds_finalize_pending. */
 int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
 /* pcs_pds2d_step restricted to the slab's own rows [ra0, rb0) u [ra1, rb1)
  * (0 <= ra0 <= rb0 <= ra1 <= rb1 <= rows): writes x', z' on those rows and one partials row per
@@ -341,9 +343,15 @@ int pcs_pds2d_step(const pcs_pds2d_args* a, hipStream_t stream);
 int64_t pcs_pds2d_nblocks_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1);
 int pcs_pds2d_step_bands(const pcs_pds2d_args* a, int64_t ra0, int64_t rb0, int64_t ra1, int64_t rb1,
                          hipStream_t stream);
-/* n iterations of pcs_pds2d_step launched back to back, ping-ponging (x, z) <-> (xn, zn)
- * (even n leaves the iterate in x, z); requires hist/ctrl/ws (in-kernel loop control).  The
- * host-side form of GenericIterativeAlgorithm.iterate's loop (pycsou/core/solver.py:55-76). */
+/* n iterations of pcs_pds2d_step launched back to back, ping-ponging (x, z) <-> (xn, zn) (and
+ * partials <-> fin_partials); requires hist/ctrl/ws (in-kernel loop control).  The host-side form of
+ * GenericIterativeAlgorithm.iterate's loop (pycsou/core/solver.py:55-76).
+ * Without fin_partials an even n leaves the iterate in (x, z).  With fin_partials (deferred
+ * finalization) the stopping rule acts one launch late: after a natural stop at iteration j the
+ * next launch has already written iterate j + 1 into the other buffer pair, and the stop flag is
+ * written mid-launch by that launch's finalizer workgroup.  The caller must then (1) call
+ * pcs_pds_finalize_pending once the run is done, before reading ctrl or hist, and (2) select the
+ * result by the parity of Ctrl.it (iterations done: even -> x, z; odd -> xn, zn), not by n. */
 int pcs_pds2d_run(const pcs_pds2d_args* a, int64_t n, hipStream_t stream);
 
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics (pycsou/opt/proxalgs.py:343-394)

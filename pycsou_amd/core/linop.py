@@ -12,6 +12,7 @@ on ``K^T K`` in O(1) vectors: every operator application and the recurrence stay
 GPU, only the small tridiagonal eigenproblem runs on the host every few steps.
 """
 
+import warnings
 from numbers import Number
 
 import numpy as np
@@ -21,7 +22,7 @@ from .. import _ops as O
 from .map import DifferentiableMap, DiffMapComp, DiffMapSum, Map, MapComp, MapSum
 
 
-def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=10, seed=0):
+def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=10, seed=0, device=None):
     """Largest eigenvalue of a PSD Gram operator (or largest |eigenvalue| of a symmetric one) by
     plain Lanczos in fp64 with O(1) memory: three vectors of ``n`` (q_prev, q, w) plus what
     ``apply`` allocates, no re-orthogonalisation (the extreme Ritz value converges regardless;
@@ -36,12 +37,16 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
     within r of the Ritz value; a Ritz value never exceeds the extreme eigenvalue, so the value
     stays on the high side of theta, which keeps tau sigma ||K||^2 <= 1 on the safe side even
     without re-orthogonalisation), and theta itself on an invariant subspace (r = 0: theta is an
-    eigenvalue of A).  The
+    eigenvalue of A).  A stagnated theta is accepted only while its residual is small too
+    (r <= sqrt(tol) |theta|, so theta + r over-estimates by at most that much): otherwise the run
+    goes on to the residual test or ``max_steps`` (ADVICE r5 -- a loose bound would shrink tau and
+    sigma below the reference's svds-based step sizes); a run that ends with a residual above that
+    warns.  The
     structured operators of the path (Gradient, derivatives, separable / 1-D convolutions) do not
     come here: their norms are exact (linop/_spectral.py).
     """
     from scipy.linalg import eigh_tridiagonal, eigvalsh_tridiagonal
-    dev = O.device()
+    dev = O.device() if device is None else device
     g = torch.Generator(device='cpu').manual_seed(seed)
     q = torch.randn(n, generator=g, dtype=torch.float64).to(dev)
     q /= torch.linalg.vector_norm(q)
@@ -84,9 +89,13 @@ def _lanczos_extreme(apply, n, sym=False, tol=1e-9, max_steps=5000, check_every=
             return theta
         if resid <= tol * abs(theta):
             return theta + resid
-        if prev is not None and abs(theta - prev) <= tol * abs(theta):
+        loose = resid > np.sqrt(tol) * abs(theta)
+        if prev is not None and abs(theta - prev) <= tol * abs(theta) and not loose:
             return theta + resid
         prev = theta
+    if resid > np.sqrt(tol) * abs(theta):
+        warnings.warn(f'Lanczos: {steps} steps left the Ritz residual at {resid / max(abs(theta), 1e-300):.2e} of '
+                      f'theta; the returned bound theta + r may over-estimate the norm by that much')
     return theta + resid
 
 

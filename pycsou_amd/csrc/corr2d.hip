@@ -357,195 +357,10 @@ __global__ __launch_bounds__(256) void k_corr2d(const T* __restrict__ x, T* __re
   }
 }
 
-// ---------------------------------------------------------------- matrix-core form (fp32, tiers 11-15)
-// v_mfma_f32_16x16x4_f32 (exact f32: each output element is an fmaf chain over k) with the taps as A
-// and one input row as B.  A tier K < 15 runs as the 15 x 15 window with its taps centred (D = 7 - K/2);
-// for input row R and a 16-column block starting at c:
-//
-//     B[k][n]     = x[R][c + n - 7 + 4s + k]           s = 0..3: the 16 column taps j = 4s + k
-//     C[m][n]    += sum_k A[m][k] B[k][n],  A[m][k] = w[i][4s + k]  with window row i = i(m, R)
-//
-// C row m (lane group m >> 2, register m & 3) is the accumulator of one output row; it takes window row
-// i = (m + R) mod 16 at input row R, i.e. i = 0, 1, ..., 15 over 16 consecutive input rows (the A operand
-// rotates through 16 phases instead of any accumulator moving), so output row r lives in C row
-// (r - 7 - R0) mod 16 and is finished at i = 15, where that register is stored and restarted at 0.  Every
-// output is therefore the one fmaf chain over (i, j) in order that k_corr2d's FMAs form (zero taps add
-// exact zeros for finite inputs), so the two kernels agree bit for bit.  (A non-finite input reaches a
-// 16 x 16 rather than K x K neighbourhood of outputs.)  For K = 15 one MFMA carries 15 x 4 of its 16 x 4
-// products (88 %, against 47 % for the Toeplitz form of DESIGN.md).
-// A wave runs CH independent 16-column chains (their MFMAs interleave, hiding the dependent-issue
-// latency); a workgroup is 4 waves marching a segment of rows in blocks of 16 input rows (the 16 A phases
-// unrolled): the block's input rows (the strip + 16 columns) land in an LDS ring one block ahead, the rows
-// finished in a block collect in an LDS buffer and leave as 16-B stores (+ beta b) in the next block.
-namespace corr2d {
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-#ifndef PCS_CORR_MF_CH  // 16-column chains per wave (diagnostics builds override)
-#define PCS_CORR_MF_CH 2
-#endif
-constexpr int kMfCH = PCS_CORR_MF_CH;
-constexpr int kMfW = 64 * kMfCH;         // columns per workgroup (4 waves x CH x 16)
-constexpr int kMfL = 8;                  // staged columns left of the strip (>= 7, 16-B aligned)
-constexpr int kMfP = kMfW + 16;          // staged input columns per row: [c0 - 8, c0 + kMfW + 8)
-constexpr int kMfBS = 16;                // input rows per block (the 16 A phases)
-}  // namespace corr2d
-
-template <int K, bool FLIP, bool VEC, bool HB>
-__global__ __launch_bounds__(256) void k_corr2d_mf(const float* __restrict__ x, float* __restrict__ out, int n0,
-                                                    int n1, const float* __restrict__ w, int ws,
-                                                    const float* __restrict__ b, float beta, int seg, int nstrips,
-                                                    int ntasks) {
-  using namespace corr2d;
-  constexpr int Kc = 7, D = 7 - K / 2, CH = kMfCH, BS = kMfBS;
-  static_assert(K <= 15 && K >= 1, "16 x 16 tap tile");
-  __shared__ __attribute__((aligned(16))) float xr[2][BS][kMfP];  // input rows, two blocks
-  __shared__ __attribute__((aligned(16))) float ob[2][BS][kMfW];  // finished rows, two blocks
-
-  int task;
-  {  // XCD-aware bijective remap (k_corr2d's)
-    const int bb = blockIdx.x, qq = ntasks / 8, rr = ntasks % 8, xcd = bb % 8, kk = bb / 8;
-    task = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + kk;
-  }
-  const int strip = task % nstrips;
-  const int r0 = (task / nstrips) * seg;
-  if (r0 >= n0) return;
-  const int r1 = min(n0, r0 + seg);
-  const int c0 = strip * kMfW;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ln = lane & 15, lg = lane >> 4;
-
-  // A operands of the 16 phases: lane (m = ln, k = lg) of tap block s, window row (m + ph) mod 16
-  float a[BS][4];
-#pragma unroll
-  for (int ph = 0; ph < BS; ++ph)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int i = ((ln + ph) & 15) - D, j = 4 * s + lg - D;
-      a[ph][s] = (i >= 0 && i < K && j >= 0 && j < K) ? tap<float, K, FLIP>(w, ws, i, j) : 0.f;
-    }
-  // resolve the tap loads here: otherwise the loop's first MFMA waits vmcnt(0), i.e. for the next
-  // block's prefetch too
-#pragma unroll
-  for (int ph = 0; ph < BS; ++ph) asm volatile("" ::"v"(a[ph][0]), "v"(a[ph][1]), "v"(a[ph][2]), "v"(a[ph][3]));
-  // input rows R = R0 + t (phase t & 15); output row R - 8 is finished at step t, so block blk finishes
-  // rows R0 - 8 + 16 blk + [0, 16); the segment runs until row r1 - 1 is finished
-  const int R0 = r0 - Kc;
-  const int nblk = ((r1 - r0) + 15 + BS - 1) / BS;
-
-  constexpr int XV = kMfP / 4, OV = kMfW / 4, NXV = BS * XV, NOV = BS * OV;
-  constexpr int NX = (NXV + 255) / 256, NO = (NOV + 255) / 256;
-  float4 px[NX], pb[NO];
-  // buffer descriptors of the whole image (host: < 1 GiB): rows / columns outside it carry kOOB and read 0
-  // (stores: are dropped) -- no branches, so no register of a pending load is ever rewritten conditionally
-  const uint32_t img = (uint32_t)n0 * (uint32_t)n1 * 4u;
-  const Rsrc rx = rsrc_of(x, img), rb = rsrc_of(b, HB ? img : 0u), ro = rsrc_of(out, img);
-  auto ld4 = [&](Rsrc r, int row, int col) -> float4 {
-    const uint32_t rof = ((unsigned)row < (unsigned)n0) ? (uint32_t)row * (uint32_t)n1 * 4u : kOOB;
-    if constexpr (VEC) {
-      const uint32_t co = ((unsigned)col < (unsigned)n1) ? (uint32_t)col * 4u : kOOB;
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(rof + co), 0, 0);
-      return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-    } else {
-      float e[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t co = ((unsigned)(col + q) < (unsigned)n1) ? (uint32_t)(col + q) * 4u : kOOB;
-        e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(rof + co), 0, 0));
-      }
-      return make_float4(e[0], e[1], e[2], e[3]);
-    }
-  };
-  // every thread issues every load (surplus ones at a kOOB row: no traffic), so no load sits in a branch
-  auto issue_b = [&](int blk) {  // b rows of the rows block blk - 1 finished
-    if constexpr (HB) {
-#pragma unroll
-      for (int q = 0; q < NO; ++q) {
-        const int e = tid + 256 * q;
-        pb[q] = ld4(rb, e < NOV && blk >= 1 ? R0 + (blk - 1) * BS - 8 + e / OV : -1, c0 + 4 * (e % OV));
-      }
-    }
-  };
-  auto issue = [&](int blk) {  // input rows of block blk, and issue_b(blk)
-    const int Rb = R0 + blk * BS;
-#pragma unroll
-    for (int q = 0; q < NX; ++q) {
-      const int e = tid + 256 * q;
-      px[q] = ld4(rx, e < NXV ? Rb + e / XV : -1, c0 - kMfL + 4 * (e % XV));
-    }
-    issue_b(blk);
-  };
-  auto land = [&](int blk) {
-#pragma unroll
-    for (int q = 0; q < NX; ++q) {
-      const int e = tid + 256 * q;
-      if (e < NXV) *reinterpret_cast<float4*>(&xr[blk & 1][e / XV][4 * (e % XV)]) = px[q];
-    }
-  };
-  // rows block blk finished (in ob[blk & 1]) -> out (+ beta b), 16-B stores
-  auto flush = [&](int blk) {
-    const int rb0 = R0 - 8 + blk * BS;
-#pragma unroll
-    for (int q = 0; q < NO; ++q) {
-      const int e = tid + 256 * q;
-      if (e < NOV) {
-        const int rr = e / OV, cv = e % OV, r = rb0 + rr, col = c0 + 4 * cv;
-        float4 o = *reinterpret_cast<const float4*>(&ob[blk & 1][rr][4 * cv]);
-        if constexpr (HB) {
-          o.x = o.x + beta * pb[q].x;
-          o.y = o.y + beta * pb[q].y;
-          o.z = o.z + beta * pb[q].z;
-          o.w = o.w + beta * pb[q].w;
-        }
-        const bool rok = r >= r0 && r < r1;
-        if constexpr (VEC) {
-          typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-          const u4 d = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
-          const uint32_t off = (rok && col < n1) ? ((uint32_t)r * (uint32_t)n1 + (uint32_t)col) * 4u : kOOB;
-          __builtin_amdgcn_raw_buffer_store_b128(d, ro, (int)off, 0, 0);
-        } else {
-          const float ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-          for (int q2 = 0; q2 < 4; ++q2) {
-            const uint32_t off =
-                (rok && col + q2 < n1) ? ((uint32_t)r * (uint32_t)n1 + (uint32_t)(col + q2)) * 4u : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ov[q2]), ro, (int)off, 0, 0);
-          }
-        }
-      }
-    }
-  };
-
-  f32x4 c[CH];
-#pragma unroll
-  for (int h = 0; h < CH; ++h) c[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int bcol = 16 * CH * wv + ln + lg + (kMfL - Kc);  // staged column of B[k = lg][n = ln], chain 0, s = 0
-  const int ocol = 16 * CH * wv + ln;                      // ob column of chain 0
-  issue(0);
-  for (int blk = 0; blk < nblk; ++blk) {
-    land(blk);
-    lds_barrier();  // block blk's rows landed; block blk - 1's finished rows complete in ob
-    if (blk >= 1) flush(blk - 1);  // (its b rows arrived with block blk's prefetch)
-    if (blk + 1 < nblk) issue(blk + 1);
-#pragma unroll
-    for (int t = 0; t < BS; ++t) {
-      // C row mf = 15 - t (lane group gf, register pf) holds window row 15 at this step: finished
-      const int mf = 15 - t, gf = mf >> 2, pf = mf & 3;
-      const float* row = &xr[blk & 1][t][bcol];
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int h = 0; h < CH; ++h)
-          c[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], row[16 * h + 4 * s], c[h], 0, 0, 0);
-#pragma unroll
-      for (int h = 0; h < CH; ++h) {
-        if (lg == gf) ob[blk & 1][t][ocol + 16 * h] = c[h][pf];
-        c[h][pf] = lg == gf ? 0.f : c[h][pf];
-      }
-    }
-  }
-  lds_barrier();
-  issue_b(nblk);  // b rows of the last block's finished rows
-  flush(nblk - 1);
-}
+// (Round 5 built a matrix-core form of this correlation -- v_mfma_f32_16x16x4_f32 with the taps as A and
+// one input row as B, bit-exact with this kernel -- and measured it slower: 0.096 against 0.089 ms per 4096^2
+// pass, profiles/r5_corr_mfma_ab.txt.  Removed from the library in round 6; the source is in git history
+// (commit e6cd0fe, k_corr2d_mf).)
 
 namespace corr2d {
 
@@ -576,51 +391,8 @@ static int slots_for() {
   return slots;
 }
 
-// the matrix-core form (PCS_CORR_MFMA=1, read per call: tests switch it inside one process).  Opt-in: at
-// 4096^2 k = 15 it runs 0.096-0.098 ms per pass against the VALU kernel's 0.089 (profiles/r5_corr_mfma_ab.txt)
-static bool use_mf() {
-  const char* e = getenv("PCS_CORR_MFMA");
-  return e && e[0] == '1';
-}
-
-template <int K, bool FLIP, bool VEC, bool HB>
-static int launch_mf(const float* x, float* out, int64_t n0, int64_t n1, const float* w, int ws, const float* b,
-                     float beta, hipStream_t st) {
-  const int64_t nstrips = (n1 + kMfW - 1) / kMfW;
-  static const int slots = [] {
-    int dev = 0, cus = 256, nb = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_corr2d_mf<K, FLIP, VEC, HB>, 256, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    (void)hipGetLastError();
-    const char* e = getenv("PCS_CORR_MF_SLOTS");  // diagnostics: workgroups per launch
-    return e && atoi(e) > 0 ? atoi(e) : cus * nb;
-  }();
-  // segments per strip: one round of the resident workgroups; a segment keeps >= 64 rows (the 15-row
-  // pipeline fill of each segment)
-  int64_t segs = slots / nstrips;
-  if (segs < 1) segs = 1;
-  int64_t seg = (n0 + segs - 1) / segs;
-  if (seg < 64) seg = 64;
-  seg = (seg + 7) / 8 * 8;
-  segs = (n0 + seg - 1) / seg;
-  const int64_t ntasks = nstrips * segs;
-  if (ntasks > 0x7fffffff) return PCS_EUNSUPPORTED;
-  k_corr2d_mf<K, FLIP, VEC, HB><<<(unsigned)ntasks, 256, 0, st>>>(x, out, (int)n0, (int)n1, w, ws, b, beta, (int)seg,
-                                                              (int)nstrips, (int)ntasks);
-  return launch_status();
-}
-
 template <typename T, int K, bool FLIP, bool VEC>
 static int launch(const T* x, T* out, int64_t n0, int64_t n1, const T* w, int ws, const T* b, T beta, hipStream_t st) {
-  // tier 15 (below, the VALU kernel's K^2 FMAs cost less than the 15 x 15 MFMA tile; the kernel takes
-  // tiers 11 / 13 centred, instantiated here for 15 only)
-  if constexpr (std::is_same<T, float>::value && K == 15) {  // descriptors over the image: < 1 GiB
-    if (use_mf() && n0 * n1 * 4 < (int64_t)kOOB)
-      return b != nullptr ? launch_mf<K, FLIP, VEC, true>(x, out, n0, n1, w, ws, b, beta, st)
-                          : launch_mf<K, FLIP, VEC, false>(x, out, n0, n1, w, ws, b, beta, st);
-  }
   using Cf = Cfg<T, K>;
   const int64_t nstrips = (n1 + Cf::TW - 1) / Cf::TW;
   const int64_t slots = slots_for<T, K, FLIP, VEC>();

@@ -402,6 +402,10 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
     load_b(bv, a + 1 + 2 * vi, true);
     load_x(xnx, a + TS + 2 * H + 1, TS);
     __builtin_amdgcn_s_setprio(0);
+    // the wait below counts the NXL x loads as issued after the z tiles and b: pin the issue order (the
+    // x rows are only consumed by store_x, so the scheduler could otherwise sink them past the wait --
+    // the hazard of the round-5 GEN race)
+    nm64_fence();
     ph(a + 2 * H + 1 + pr);
     __builtin_amdgcn_s_waitcnt((NXL & 15) | ((NXL >> 4) << 14) | (7 << 4) | (15 << 8));  // z tiles and b landed
     lds_barrier();

@@ -154,35 +154,6 @@ def test_conv2d_raw_tiers(A, dtype, k, shape):
     assert rel(host(out), ref.rmatvec(x.astype(np.float64))) < 10 * TOL[dtype]
 
 
-@pytest.mark.parametrize('k', [15])
-@pytest.mark.parametrize('shape', [(64, 64), (37, 130), (300, 7), (1, 1), (1000, 4096), (517, 1001)])
-def test_conv2d_mfma_bitwise_vs_valu(A, monkeypatch, k, shape):
-    """The opt-in matrix-core correlation for fp32 tier 15 (PCS_CORR_MFMA=1, k_corr2d_mf:
-    v_mfma_f32_16x16x4_f32 with the taps as A, one input row as B, the A operand rotating through 16
-    phases): every output is the same fmaf chain over (i, j) as the VALU kernel's, so forward + fused
-    residual and adjoint agree bit for bit -- ragged widths (scalar loads), one-row images, many
-    segments."""
-    from pycsou_amd import _lib as L
-    lib = L.gpu()
-    rng = np.random.default_rng(100 + k)
-    h = rng.standard_normal((k, k)).astype(np.float32)
-    N = shape[0] * shape[1]
-    xd, yd = dev(rng.standard_normal(N).astype(np.float32)), dev(rng.standard_normal(N).astype(np.float32))
-    hd, hfd = dev(h), dev(np.ascontiguousarray(h[::-1, ::-1]))
-    res = []
-    for mf in ('1', '0'):
-        monkeypatch.setenv('PCS_CORR_MFMA', mf)
-        o1, o2 = torch.empty_like(xd), torch.empty_like(xd)
-        assert lib.pcs_conv2d(L.PCS_F32, L.ptr(xd), L.ptr(o1), shape[0], shape[1], L.ptr(hd), k, k, k // 2, k // 2,
-                              L.ptr(yd), -1.0, L.stream()) == 0
-        assert lib.pcs_conv2d(L.PCS_F32, L.ptr(xd), L.ptr(o2), shape[0], shape[1], L.ptr(hfd), k, k, k // 2, k // 2,
-                              None, 0.0, L.stream()) == 0
-        torch.cuda.synchronize()
-        res.append((o1, o2))
-    assert torch.equal(res[0][0], res[1][0]), (res[0][0] - res[1][0]).abs().max().item()
-    assert torch.equal(res[0][1], res[1][1]), (res[0][1] - res[1][1]).abs().max().item()
-
-
 @pytest.mark.parametrize('dtype', [np.float64, np.float32])
 @pytest.mark.parametrize('kshape', [(15, 15), (6, 11), (1, 30)])
 @pytest.mark.parametrize('shape', [(1000, 4096), (517, 1023), (130, 64)])

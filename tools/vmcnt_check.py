@@ -1,38 +1,75 @@
-"""Static check of the row-march kernels' LDS-DMA waits (round 5): in the main loop of every
-k_pds2d_nmarch* kernel of an assembly file (hipcc -S), the `s_waitcnt vmcnt(N)` before the barrier that
-precedes the first read of the z tiles must see at least N plain loads issued after the step's last
-`buffer_load ... lds`; otherwise a DMA load may still be in flight when the tile is read."""
+"""Static check of the LDS-DMA waits (round 5; every DMA site since round 6).
+
+Every kernel of an assembly file (hipcc -S) that issues `buffer_load ... lds` is scanned site by
+site: the DMA loads between two `s_waitcnt vmcnt` are one group, and the first `s_barrier` after the
+group that follows a vmcnt wait is the one that publishes the group's LDS tile.  Before that barrier
+some `s_waitcnt vmcnt(N)` must see at least N vector-memory loads issued after the group's last DMA
+load; otherwise a DMA load may still be in flight when the tile is read.  A kernel whose loop the
+compiler inlined several times (peeled prologue, interior-only loop, mixed loop) has one group per
+copy, and each is checked -- a single-site check (the round-5 form) only saw the textually last one."""
 import re
 import sys
 
+_WAIT = re.compile(r's_waitcnt\b.*\bvmcnt\((\d+)\)')
 
-def check(path):
+
+def _is_dma(l):
+    return l.startswith('buffer_load') and l.endswith(' lds')
+
+
+def _is_vmem_load(l):
+    return (l.startswith('buffer_load') or l.startswith('global_load')) and not l.endswith(' lds')
+
+
+def check_body(body):
+    """[(site index, ok, wait N, loads after the group)] for every DMA group of one kernel body."""
+    out = []
+    i, n = 0, len(body)
+    while i < n:
+        if not _is_dma(body[i]):
+            i += 1
+            continue
+        # the group: DMA loads until the next vmcnt wait (other instructions may sit between them)
+        last, j = i, i + 1
+        while j < n and not _WAIT.search(body[j]) and not body[j].startswith('s_barrier'):
+            if _is_dma(body[j]):
+                last = j
+            j += 1
+        n_after, waits, verdict = 0, [], None
+        for l in body[last + 1:]:
+            if _is_vmem_load(l):
+                n_after += 1
+            m = _WAIT.search(l)
+            if m:
+                waits.append((int(m.group(1)), n_after))
+            if l.startswith('s_barrier') and waits:
+                ok = any(w <= a for w, a in waits)
+                verdict = (ok, min(w for w, _ in waits), n_after)
+                break
+        if verdict is None:
+            verdict = (False, None, n_after)
+        out.append((last,) + verdict)
+        i = last + 1
+    return out
+
+
+def check(path, pattern=r'^_Z\w+:'):
     lines = open(path).read().split('\n')
-    starts = [i for i, l in enumerate(lines) if re.match(r'^_ZN3pcs\w*k_pds2d_nmarch\w*:', l)]
+    starts = [i for i, l in enumerate(lines) if re.match(pattern, l)]
     bad = 0
     for s in starts:
         name = lines[s].split(':')[0]
         e = s + 1
-        while not lines[e].startswith('.Lfunc_end'):
+        while e < len(lines) and not lines[e].startswith('.Lfunc_end'):
             e += 1
         body = [l.strip() for l in lines[s:e]]
-        dma = [i for i, l in enumerate(body) if l.startswith('buffer_load') and l.endswith(' lds')]
-        if not dma:
+        sites = check_body(body)
+        if not sites:
             continue
-        last = dma[-1]
-        n_after, verdict = 0, None
-        for l in body[last + 1:]:
-            if l.startswith('buffer_load') and not l.endswith(' lds'):
-                n_after += 1
-            m = re.match(r's_waitcnt vmcnt\((\d+)\)', l)
-            if m:
-                n = int(m.group(1))
-                verdict = (n, n_after)
-            if l.startswith('s_barrier') and verdict is not None:
-                break
-        ok = verdict is not None and verdict[1] >= verdict[0]
-        bad += not ok
-        print(('ok  ' if ok else 'RACE'), name[:70], 'wait vmcnt', verdict[0] if verdict else None, 'loads after DMA', n_after)
+        nbad = sum(not ok for _, ok, _, _ in sites)
+        bad += nbad
+        detail = ' '.join(f'[{w}<={a}]' if ok else f'[RACE {w}>{a}]' for _, ok, w, a in sites)
+        print(('ok  ' if not nbad else 'RACE'), name[:70], f'{len(sites)} DMA sites', detail)
     return bad
 
 
