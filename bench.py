@@ -273,6 +273,31 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
     probe = comm_probe(eng) if world > 1 else None
     ms = dt * 1e3 / K
     elem = torch.empty(0, dtype=dtype).element_size()
+    # the launches of one iteration timed apart (HIP events, eager, after the timed region) and the
+    # roofline of each: algorithmic words per voxel -- nrm: read x, write t (2); conv0: read t and
+    # C12^T y, write g (3); update: x, g, z (3) in, x', z' (3) out (9), with the axis-0 pass folded in
+    # x, t, C12^T y, z (3) in (10)
+    parts, roof = None, None
+    if world == 1:
+        parts = eng.time_parts(3)
+        fold = bool(getattr(eng, 'fold', False))
+        words = {'nrm': 2, 'conv0': 3, 'step': 10 if fold else 9}
+        upd = 'k_pds3d' if kind == 'forward' else 'k_pds3d_gen'
+        names = {'nrm': f'k_sep2d_{"nrm" if elem == 4 else "nrmm"}<{"float" if elem == 4 else "double"}>',
+                 'conv0': f'k_conv0_rta<{"float" if elem == 4 else "double"},15>',
+                 'step': f'{upd}<{"float" if elem == 4 else "double"}{", PCS_F_CONV0" if fold else ""}>'}
+        per = {}
+        for k, t in parts.items():
+            if k in words:
+                gbs = words[k] * n ** 3 * elem / (t * 1e-3) / 1e9
+                per[k] = {'kernel': names[k], 'kernel_ms': round(t, 4), 'words_per_voxel': words[k],
+                          'achieved': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 4)}
+        if 'step' in per:
+            s = per['step']
+            roof = {'bound': 'hbm', 'kernel': s['kernel'], 'kernel_ms': s['kernel_ms'], 'achieved': s['achieved'],
+                    'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': s['frac'], 'parts': per,
+                    'words_per_voxel_iteration': sum(words[k] for k in per),
+                    'source': 'HIP-event pairs around each launch of 3 eager iterations after the timed region'}
     alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
     halo = 0 if world == 1 else (eng.hx + 3 * eng.hz) * eng.plane * elem
     res = {'workload': f'{"C5" if elem == 8 else "C4"} 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
@@ -289,6 +314,7 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
                            if world > 1 else None,
            'order_trial_ms': getattr(eng, 'tune_ms', None),
            'comm': probe,
+           'roofline': roof,
            'setup_s': round(t1 - t0, 1)}
     del eng
     if comm is not None:
@@ -697,6 +723,82 @@ def slab_bench(n, dtype, K, W, world):
             'comm': probe}
 
 
+def strong_bench(n, dtype, K, W, world, depths=(1, 2, 4, 8)):
+    """The metric as written (BASELINE: 'PDS iters/sec on 4096^2 TV-deconv ... at 1/2/4/8 GPU'): ONE n x n
+    image split into `world` row slabs (strong scaling), the native RCCL loop.  Depth 1 is the
+    per-iteration exchange (serial / overlapped schedule trial); depth k > 1 the communication-avoiding
+    loop (pcs_slab2d_deep_run: halos k iterations deep, one all-gather + exchange per k iterations, the
+    shrinking halo rows recomputed locally).  Each depth is timed over 2 chunks of 16 iterations through
+    the real transport (max over ranks) and the fastest runs the W + K measurement; the trial times are
+    reported.  gloo rehearsals (no RCCL) run depth 1 on the torch.distributed loop only."""
+    from pycsou_amd.parallel import DistComm, SlabPDS2D
+    from pycsou_amd.parallel.slab import comm_probe, row_split
+    pds = build_problem(n, n, dtype, lipschitz='analytic')
+    comm = DistComm()
+    native = dist.get_backend() == 'nccl'
+    rank = comm.rank
+    rows = row_split(n, world, rank)[1]
+    trials, best, best_ms = {}, None, None
+
+    def timed(eng, iters):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        eng.advance(iters)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device='cuda' if native else 'cpu')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) * 1e3 / iters
+
+    for d in (depths if native else (1,)):
+        try:
+            eng = SlabPDS2D.from_pds(pds, comm, native=native, depth=d)
+        except ValueError as e:  # a slab thinner than the deep halo: that depth does not apply
+            trials[d] = f'skipped: {e}'[:120]
+            continue
+        if d == 1 and native:
+            eng.overlapped()
+        total = 64 + W + K
+        eng.init_loop(total, total, -1.0)
+        eng.advance(16)  # untimed (plan creation; depth 1: its schedule trial)
+        ms = timed(eng, 32)
+        trials[d] = round(ms, 4)
+        if best_ms is None or ms < best_ms:
+            if best is not None:
+                best._destroy_plan()
+            best, best_ms = eng, ms
+        else:
+            eng._destroy_plan()
+            del eng
+    eng = best
+    total = W + K + 4
+    eng.init_loop(total, total, -1.0)
+    eng.advance(W)
+    ms = timed(eng, K)
+    assert eng.iterations() == W + K, (eng.iterations(), W, K)
+    probe = comm_probe(eng)
+    elem = 4 if dtype == torch.float32 else 8
+    alg = 7 * n * n * elem  # the whole image's (2d+3) N words per iteration, all ranks together
+    res = {'workload': f'C3 TV-deconvolution {n}x{n} (ONE image, {world} row slabs of ~{rows} rows: strong scaling), '
+                       f'15x15 Gaussian PSF, Gradient(forward), 0.05*L21Norm, fused normal-operator march per slab',
+           'it_per_s': round(1e3 / ms, 2), 'ms_per_iter': round(ms, 5), 'steps': K, 'warmup': W,
+           'depth': eng.depth, 'depth_trial_ms_per_iter': trials,
+           'loop': ('native deep-halo (pcs_slab2d_deep_run)' if eng.depth > 1 else
+                    ('native, overlapped' if eng.native and eng.overlapped() else
+                     'native, serial' if eng.native else 'python (gloo rehearsal)')),
+           'iteration_GBps': round(alg / (ms * 1e-3) / 1e9, 1),
+           'iteration_frac_of_hbm_peak_per_gpu': round(alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
+           'alg_bytes_per_iter': alg, 'comm': probe, 'scaling': 'strong'}
+    if probe is not None and eng.depth > 1:
+        probe['per'] = f'one chunk of {eng.depth} iterations (all-gather of {4 * eng.depth} sums, deep-halo exchange)'
+    eng._destroy_plan()
+    del eng, best, pds
+    comm.close()
+    torch.cuda.empty_cache()
+    return res
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -792,7 +894,7 @@ def main():
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
     ap.add_argument('--cpu-iters', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:20,c4_cen:512:f32:20:centered',
+    ap.add_argument('--volumes', default='c4:512:f32:20,c5:1024:f64:20,c4_cen:512:f32:20:centered,c5_cen:1024:f64:20:centered',
                     help='volume legs name:edge:dtype:steps[:kind], comma separated ("" skips them)')
     ap.add_argument('--volume-timeout', type=float, default=240.0)
     ap.add_argument('--legs', default='c2,c3_nonsep,c2_lap,c2_cen,c3_cen,c3_f64,c3_cen_f64,conv63,cps_inpaint',
@@ -805,6 +907,8 @@ def main():
                     help='slab: run the row-slab (multi-GPU) engine even at N=1 (diagnostics)')
     ap.add_argument('--headline-timeout', type=float, default=420.0,
                     help='watchdog (s) on the N > 1 slab headline: a stall prints the line with an error and exits 1')
+    ap.add_argument('--no-strong', dest='strong', action='store_false',
+                    help='N > 1: skip the strong-scaling entry (one --size^2 image split over the N ranks)')
     ap.add_argument('--launch-check', action='store_true',
                     help='start the ranks, join the process group, all-reduce once and print the launch facts '
                          '(no GPU work; with PCS_BENCH_BACKEND=gloo it runs on a host without GPUs)')
@@ -940,6 +1044,15 @@ def main():
         out = volume_leg(args, out if rank == 0 else None, f'volume_{name}', int(edge),
                          torch.float64 if vdt == 'f64' else torch.float32, int(vsteps), world, rank,
                          vk[0] if vk else 'forward')
+    if world > 1 and args.strong:
+        # the metric as written: one 4096^2 image over the N ranks (strong scaling), beside the weak headline
+        try:
+            sres = strong_bench(args.size, dtype, K, W, world)
+        except Exception as e:  # noqa: BLE001 -- the headline line stands on its own
+            sres = {'error': f'{type(e).__name__}: {e}'[:300]}
+            print(f'bench: strong-scaling entry failed: {sres["error"]}', file=sys.stderr)
+        if rank == 0:
+            out['strong_4096'] = sres
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

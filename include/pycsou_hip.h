@@ -437,6 +437,40 @@ int pcs_slab2d_overlapped(const void* plan);
 int pcs_slab2d_run(void* plan, int64_t n, int p0, hipStream_t stream);
 int pcs_slab2d_destroy(void* plan);
 
+/* Communication-avoiding form of the row-slab loop (ABI 9; the same iteration as pcs_slab2d_run,
+ * GenericIterativeAlgorithm.iterate of pycsou/core/solver.py:55-76 across ranks): the halos of x, z, y
+ * are stored `depth` iterations deep and exchanged once per chunk of `depth` iterations.  Iteration j of
+ * a chunk computes the own rows plus (m - j) * reach redundant rows of each halo (clipped at the image),
+ * so the own rows after the chunk are bitwise the single-GPU iterate; the m x 4 norm sums of a chunk are
+ * all-gathered once and pcs_pds_reduce_finalize_k runs the loop control over them in iteration order.
+ * Buffers rotate through nbuf sets (step[b]: X[b] -> X[(b + 1) % nbuf]); after n iterations from set 0
+ * the iterate is set n % nbuf, and after a natural stop set (Ctrl.it % nbuf).  Needs the banded
+ * (row-marching) step: PCS_EUNSUPPORTED at create otherwise. */
+#define PCS_DEEP_MAX 8
+typedef struct {
+  int world, rank;
+  int depth;              /* 1 <= depth <= PCS_DEEP_MAX: iterations per exchange */
+  int nbuf;               /* buffer sets in the rotation, >= max(2, depth) */
+  int reach;              /* even, >= the rows one iteration reads past its own (x and z) */
+  int local;              /* 1: no communicator -- the plan runs only under pcs_slab2d_deep_run_local */
+  pcs_pds2d_args step[PCS_DEEP_MAX]; /* plain slabs with the deep halos (>= (depth - 1) reach + 1 rows) */
+  pcs_halo_set halo[PCS_DEEP_MAX];   /* the deep halos of X[b], Z[b] */
+  void* ctrl;
+  double* hist;
+} pcs_slab2d_deep_desc;
+int pcs_slab2d_deep_create(const pcs_slab2d_deep_desc* d, void* comm, void** plan);
+/* n iterations from buffer set b0: chunks of depth (the last one shorter), each followed by the
+ * all-gather, the loop control and the deep-halo exchange. */
+int pcs_slab2d_deep_run(void* plan, int64_t n, int b0, hipStream_t stream);
+/* The same chunks for all `nplans` ranks of one image in ONE process (plans[i] of ranks 0..nplans-1,
+ * one stream): the all-gather and the halo exchange as device copies -- the parity tests' transport. */
+int pcs_slab2d_deep_run_local(void* const* plans, int nplans, int64_t n, int b0, hipStream_t stream);
+int pcs_slab2d_deep_destroy(void* plan);
+/* Loop control over k iterations' sums gathered as [world][k][4] (rank r's k rows of 4 sums, each summed
+ * across ranks in the order pcs_pds_reduce_finalize uses), in iteration order. */
+int pcs_pds_reduce_finalize_k(const double* gathered, int world, int k, void* ctrl_dev, double* hist,
+                              hipStream_t stream);
+
 /* One fused PrimalDualSplitting.update_iterand + update_diagnostics for 3-D volumes
  * (pycsou/opt/proxalgs.py:343-394), K = Gradient(kind='forward') in 3-D
  * (pycsou/linop/diff.py:777-882): the same update as pcs_pds2d_step with three gradient

@@ -85,6 +85,15 @@ class Slab2DDesc(ctypes.Structure):
                 ('ctrl', _vp), ('hist', _vp), ('band', _c_i64), ('overlap', _c_int), ('pad2', _c_int)]
 
 
+DEEP_MAX = 8
+
+
+class SlabDeepDesc(ctypes.Structure):
+    """Mirror of pcs_slab2d_deep_desc (ABI 9)."""
+    _fields_ = [('world', _c_int), ('rank', _c_int), ('depth', _c_int), ('nbuf', _c_int), ('reach', _c_int),
+                ('local', _c_int), ('step', PdsArgs * DEEP_MAX), ('halo', HaloSet * DEEP_MAX), ('ctrl', _vp),
+                ('hist', _vp)]
+
 # name -> (restype, argtypes)
 _SIGS = {
     'pcs_abi_version': (_c_int, []),
@@ -158,6 +167,11 @@ _SIGS = {
     'pcs_slab2d_overlapped': (_c_int, [_vp]),
     'pcs_slab2d_run': (_c_int, [_vp, _c_i64, _c_int, _vp]),
     'pcs_slab2d_destroy': (_c_int, [_vp]),
+    'pcs_slab2d_deep_create': (_c_int, [ctypes.POINTER(SlabDeepDesc), _vp, ctypes.POINTER(_vp)]),
+    'pcs_slab2d_deep_run': (_c_int, [_vp, _c_i64, _c_int, _vp]),
+    'pcs_slab2d_deep_run_local': (_c_int, [ctypes.POINTER(_vp), _c_int, _c_i64, _c_int, _vp]),
+    'pcs_slab2d_deep_destroy': (_c_int, [_vp]),
+    'pcs_pds_reduce_finalize_k': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp]),
     'pcs_pds3d_nblocks': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_ws_bytes': (_c_i64, [ctypes.POINTER(Pds3Args)]),
     'pcs_pds3d_step': (_c_int, [ctypes.POINTER(Pds3Args), _vp]),
@@ -182,7 +196,7 @@ class HipError(ValueError):
 
 
 # the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 def load():

@@ -78,6 +78,26 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_finalize(const double* _
   if (threadIdx.x == 0) finalize_from(v, c, hist);
 }
 
+// k iterations' norm sums gathered from `world` ranks as [world][k][4] (the deep-halo slab loop's one
+// all-gather per chunk): iteration j's rank rows summed exactly as k_reduce_finalize sums a contiguous
+// [world][4] (lane r holds rank r's row, then the block tree), then the loop control, in iteration order.
+// Thread 0 alone runs finalize_from and tests the stop flag it wrote itself; iterations after a stop are
+// not recorded (solver.py:65-66).
+__global__ __launch_bounds__(kRedThreads) void k_reduce_finalize_k(const double* __restrict__ g, int world, int k,
+                                                                   Ctrl* c, double* hist) {
+  __shared__ double red[4 * (kRedThreads / 64)];
+  for (int j = 0; j < k; ++j) {
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if ((int)threadIdx.x < world) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = g[((int64_t)threadIdx.x * k + j) * 4 + q];
+    }
+    block_sum<4>(v, red);
+    if (threadIdx.x == 0 && !c->stopped) finalize_from(v, c, hist);
+    __syncthreads();  // red reused by the next iteration's tree
+  }
+}
+
 __global__ __launch_bounds__(kFinLanes) void k_finalize_pending(const double* __restrict__ part, int64_t np, Ctrl* c,
                                                                 double* hist) {
   __shared__ double red[4 * (kFinLanes / 64)];
@@ -444,6 +464,12 @@ int pcs_pds_finalize(const double* sums, void* ctrl, double* hist, hipStream_t s
 int pcs_pds_finalize_pending(const double* part, int64_t np, void* ctrl, double* hist, hipStream_t st) {
   if (!part || !ctrl || !hist || np < 1) return PCS_EINVAL;
   k_finalize_pending<<<1, kFinLanes, 0, st>>>(part, np, (Ctrl*)ctrl, hist);
+  return launch_status();
+}
+
+int pcs_pds_reduce_finalize_k(const double* gathered, int world, int k, void* ctrl, double* hist, hipStream_t st) {
+  if (!gathered || !ctrl || !hist || world < 1 || world > kRedThreads || k < 1) return PCS_EINVAL;
+  k_reduce_finalize_k<<<1, kRedThreads, 0, st>>>(gathered, world, k, (Ctrl*)ctrl, hist);
   return launch_status();
 }
 

@@ -124,6 +124,36 @@ __device__ __forceinline__ void gstore(T* p, const G4<T>& g, int c, int n2) {
   }
 }
 
+// LDS tiles of 4-groups with a row pitch of W elements.  fp32: plain rows (group g of row r at r W + 4 g).
+// fp64: every row is stored as two half-rows of W / 2 doubles -- half h of group g (its elements 2 h, 2 h + 1)
+// at (2 r + h) W / 2 + 2 g -- so the two 16-B reads / writes of a group by consecutive lanes on consecutive
+// groups are each contiguous (ds_read_b128 / ds_write_b128 without bank conflicts).  The plain layout's 32-B
+// lane stride cost 0.85 G (forward K) / 1.18 G (centred K) bank-conflict cycles per C5 update launch
+// (profiles/r6_prof_c5*).
+template <int W>
+__device__ __forceinline__ G4<float> tl_ld(const float* a, int r, int g) {
+  return lds4(a + r * W + 4 * g);
+}
+template <int W>
+__device__ __forceinline__ void tl_st(float* a, int r, int g, const G4<float>& v) {
+  st4(a + r * W + 4 * g, v);
+}
+template <int W>
+__device__ __forceinline__ G4<double> tl_ld(const double* a, int r, int g) {
+  static_assert(W % 4 == 0, "16-B aligned half-rows");
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const volatile d2* lds_d2;
+  const double* p = a + 2 * r * (W / 2) + 2 * g;
+  const d2 lo = *(lds_d2)(p), hi = *(lds_d2)(p + W / 2);
+  return {{lo.x, lo.y, hi.x, hi.y}};
+}
+template <int W>
+__device__ __forceinline__ void tl_st(double* a, int r, int g, const G4<double>& v) {
+  double* p = a + 2 * r * (W / 2) + 2 * g;
+  *reinterpret_cast<double2*>(p) = make_double2(v.v[0], v.v[1]);
+  *reinterpret_cast<double2*>(p + W / 2) = make_double2(v.v[2], v.v[3]);
+}
+
 #ifndef PCS_K3TW
 #define PCS_K3TW 128
 #endif
@@ -311,9 +341,9 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
     z2r = gload<T, VEC>(rz2, off_z2);
   };
   auto land = [&](int slot) {
-    if (tid < NU) st4(&Z0[slot][ui * WG + 4 * ug], z0r);
-    if (tid < NZ1) st4(&Z1[slot][e1r * WG + 4 * e1g], z1r);
-    if (tid < NZ2) st4(&Z2[slot][e2r * (WG + 4) + 4 * e2g], z2r);
+    if (tid < NU) tl_st<WG>(Z0[slot], ui, ug, z0r);
+    if (tid < NZ1) tl_st<WG>(Z1[slot], e1r, e1g, z1r);
+    if (tid < NZ2) tl_st<WG + 4>(Z2[slot], e2r, e2g, z2r);
   };
 
   double part[4] = {0.0, 0.0, 0.0, 0.0};
@@ -370,7 +400,7 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
   {
     const Rsrc rz0 = plane_rsrc(z, v, v.hz, p_start - 1);
     const G4<T> zp = gload<T, VEC>(rz0, off_u);
-    if (tid < NU) st4(&Z0[(p_start - 1) & 1][ui * WG + 4 * ug], zp);
+    if (tid < NU) tl_st<WG>(Z0[(p_start - 1) & 1], ui, ug, zp);
   }
   prefetch(p_start);
   for (int p = p_start; p <= p_end; ++p) {
@@ -394,12 +424,12 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
     if (!FOLD || u_wave) {  // every thread runs an item (surplus threads redo the last one; only
       // real items store); with FOLD the waves without real items skip it
       if constexpr (FOLD) gv4 = lds4(&GS[slot][ui * WG + 4 * ug]);  // g(p)
-      const G4<T> zb = lds4(&Z0[slot][ui * WG + 4 * ug]);         // z0(p)
-      const G4<T> za = lds4(&Z0[prev][ui * WG + 4 * ug]);         // z0(p-1)
-      const G4<T> z1a = lds4(&Z1[slot][ui * WG + 4 * ug]);        // z1(p, i1-1)
-      const G4<T> z1b = lds4(&Z1[slot][(ui + 1) * WG + 4 * ug]);  // z1(p, i1)
-      const G4<T> z2a = lds4(&Z2[slot][ui * (WG + 4) + 4 * ug]);  // z2(p, c-4 .. c-1)
-      const G4<T> z2b = lds4(&Z2[slot][ui * (WG + 4) + 4 * ug + 4]);
+      const G4<T> zb = tl_ld<WG>(Z0[slot], ui, ug);           // z0(p)
+      const G4<T> za = tl_ld<WG>(Z0[prev], ui, ug);           // z0(p-1)
+      const G4<T> z1a = tl_ld<WG>(Z1[slot], ui, ug);          // z1(p, i1-1)
+      const G4<T> z1b = tl_ld<WG>(Z1[slot], ui + 1, ug);      // z1(p, i1)
+      const G4<T> z2a = tl_ld<WG + 4>(Z2[slot], ui, ug);      // z2(p, c-4 .. c-1)
+      const G4<T> z2b = tl_ld<WG + 4>(Z2[slot], ui, ug + 1);
       const bool rin = fl & 1, gin = fl & 2, glast = fl & 4, rlast = fl & 8;
       const bool p_first = gp <= 0, p_last = gp >= v.n0 - 1;
       const bool in = rin && gin && gp >= 0 && gp < v.n0 && p <= v.planes;
@@ -439,7 +469,7 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
         part[1] += (double)sx;
         gstore<T, VEC>(xn + (int64_t)(p + v.hx) * pl + (int64_t)i1u * v.n2 + c_u, xo, c_u, v.n2);
       }
-      if (tid < NU) st4(&U[slot][ui * WG + 4 * ug], uo);
+      if (tid < NU) tl_st<WG>(U[slot], ui, ug, uo);
     }
     lds_barrier();
     // ---- z' items for plane p - 1 (own tile)
@@ -447,13 +477,13 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
       const int q = p - 1, gq = gp - 1;
       const bool rin = fl & 16, gin = fl & 32, glast = fl & 64, rlast = fl & 128;
       const bool own = rin && gin && gq < v.n0;
-      const G4<T> uc = lds4(&U[prev][zi * WG + 4 * zg]);
-      const G4<T> un = lds4(&U[prev][zi * WG + 4 * zg + 4]);
-      const G4<T> ud = lds4(&U[prev][(zi + 1) * WG + 4 * zg]);
-      const G4<T> up = lds4(&U[slot][zi * WG + 4 * zg]);  // u(p)
-      const G4<T> zv0 = lds4(&Z0[prev][zi * WG + 4 * zg]);
-      const G4<T> zv1 = lds4(&Z1[prev][(zi + 1) * WG + 4 * zg]);
-      const G4<T> zv2 = lds4(&Z2[prev][zi * (WG + 4) + 4 * zg + 4]);
+      const G4<T> uc = tl_ld<WG>(U[prev], zi, zg);
+      const G4<T> un = tl_ld<WG>(U[prev], zi, zg + 1);
+      const G4<T> ud = tl_ld<WG>(U[prev], zi + 1, zg);
+      const G4<T> up = tl_ld<WG>(U[slot], zi, zg);  // u(p)
+      const G4<T> zv0 = tl_ld<WG>(Z0[prev], zi, zg);
+      const G4<T> zv1 = tl_ld<WG>(Z1[prev], zi + 1, zg);
+      const G4<T> zv2 = tl_ld<WG + 4>(Z2[prev], zi, zg + 1);
       const bool q_last = gq >= v.n0 - 1;
       G4<T> o0, o1, o2;
       T sdz = T(0), sz = T(0);
@@ -621,13 +651,13 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
     constexpr int S = decltype(sc)::value;
 #pragma unroll
     for (int k = 0; k < KU; ++k)
-      if (k * NT + tid < NU) st4(&Z0[s3][ui[k] * WU + 4 * ug[k]], z0r[S][k]);
+      if (k * NT + tid < NU) tl_st<WU>(Z0[s3], ui[k], ug[k], z0r[S][k]);
 #pragma unroll
     for (int k = 0; k < K1; ++k)
-      if (k * NT + tid < NZ1) st4(&Z1[s2][(k * NT + tid) * 4], z1r[S][k]);  // row-major, pitch WU
+      if (k * NT + tid < NZ1) tl_st<WU>(Z1[s2], (k * NT + tid) / UG, (k * NT + tid) % UG, z1r[S][k]);
 #pragma unroll
     for (int k = 0; k < K2; ++k)
-      if (k * NT + tid < NZ2) st4(&Z2[s2][(k * NT + tid) * 4], z2r[S][k]);  // row-major, pitch W2
+      if (k * NT + tid < NZ2) tl_st<W2>(Z2[s2], (k * NT + tid) / W2G, (k * NT + tid) % W2G, z2r[S][k]);
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
@@ -643,7 +673,7 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
 #pragma unroll
       for (int k = 0; k < KU; ++k) {
         const G4<T> zz = gload<T, VEC>(r0, off_u[k]);
-        if (k * NT + tid < NU) st4(&Z0[slot3(pa + j)][ui[k] * WU + 4 * ug[k]], zz);
+        if (k * NT + tid < NU) tl_st<WU>(Z0[slot3(pa + j)], ui[k], ug[k], zz);
       }
     }
   }
@@ -672,12 +702,11 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
         for (int k = 0; k < KU; ++k) {
           if (k * NT + tid >= NU) continue;
           const int i1 = r1 - 1 + ui[k], c = c2 - 4 + 4 * ug[k];
-          const int o = ui[k] * WU + 4 * ug[k];
-          const G4<T> za = lds4(&Z0[sm1][o]), zb = lds4(&Z0[s0][o]), zc = lds4(&Z0[sp1][o]);
-          const int o1 = (ui[k] + 1) * WU + 4 * ug[k];  // z1 region row of i1
-          const G4<T> y0 = lds4(&Z1[b2][o1 - WU]), y1 = lds4(&Z1[b2][o1]), y2 = lds4(&Z1[b2][o1 + WU]);
-          const int o2 = ui[k] * W2 + 4 * (ug[k] + 1);  // z2 region group of c
-          const G4<T> wl = lds4(&Z2[b2][o2 - 4]), wc = lds4(&Z2[b2][o2]), wr = lds4(&Z2[b2][o2 + 4]);
+          const int ur = ui[k], uq = ug[k];
+          const G4<T> za = tl_ld<WU>(Z0[sm1], ur, uq), zb = tl_ld<WU>(Z0[s0], ur, uq), zc = tl_ld<WU>(Z0[sp1], ur, uq);
+          // z1 region rows ur .. ur + 2 = rows i1 - 1 .. i1 + 1; z2 region groups uq .. uq + 2 = c - 4 .. c + 7
+          const G4<T> y0 = tl_ld<WU>(Z1[b2], ur, uq), y1 = tl_ld<WU>(Z1[b2], ur + 1, uq), y2 = tl_ld<WU>(Z1[b2], ur + 2, uq);
+          const G4<T> wl = tl_ld<W2>(Z2[b2], ur, uq), wc = tl_ld<W2>(Z2[b2], ur, uq + 1), wr = tl_ld<W2>(Z2[b2], ur, uq + 2);
           const T h2[6] = {wl.v[3], wc.v[0], wc.v[1], wc.v[2], wc.v[3], wr.v[0]};
           const bool rin = (unsigned)i1 < (unsigned)v.n1, pin = gp >= 0 && gp < v.n0;
           const bool own = rin && pin && ui[k] >= 1 && ui[k] <= T1 && ug[k] >= 1 && ug[k] <= TW / 4 && c < v.n2 &&
@@ -713,7 +742,7 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
             part[1] += (double)sx;
             gstore<T, VEC>(xn + (int64_t)(p + v.hx) * pl + (int64_t)i1 * v.n2 + c, xo, c, v.n2);
           }
-          st4(&U[s0][o], uo);
+          tl_st<WU>(U[s0], ur, uq, uo);
         }
       };
       // three forms: interior; the edge rules on the row and column axes only (the tiles along the plane's
@@ -732,14 +761,15 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
         constexpr bool I0 = decltype(ic0)::value, I1 = decltype(ic12)::value, I2 = decltype(ic2)::value;
         if (p > p_start && tid < NZ) {
           const int q = p - 1, gq = gp - 1;
-          const int o = (zi + 1) * WU + 4 * (zg + 1);
-          const G4<T> ua = lds4(&U[sm2][o]), ub = lds4(&U[sm1][o]), uc = lds4(&U[s0][o]);  // u(q-1), u(q), u(q+1)
-          const G4<T> un = lds4(&U[sm1][o - WU]), us = lds4(&U[sm1][o + WU]);             // rows i1-1, i1+1
-          const G4<T> ul = lds4(&U[sm1][o - 4]), ur = lds4(&U[sm1][o + 4]);               // groups left / right
+          const int orr = zi + 1, og = zg + 1;  // the u region's row / group of the item
+          const G4<T> ua = tl_ld<WU>(U[sm2], orr, og), ub = tl_ld<WU>(U[sm1], orr, og),
+                      uc = tl_ld<WU>(U[s0], orr, og);                                         // u(q-1), u(q), u(q+1)
+          const G4<T> un = tl_ld<WU>(U[sm1], orr - 1, og), us = tl_ld<WU>(U[sm1], orr + 1, og);  // rows i1-1, i1+1
+          const G4<T> ul = tl_ld<WU>(U[sm1], orr, og - 1), ur = tl_ld<WU>(U[sm1], orr, og + 1);  // groups left / right
           const T h2[6] = {ul.v[3], ub.v[0], ub.v[1], ub.v[2], ub.v[3], ur.v[0]};
-          const G4<T> zv0 = lds4(&Z0[sm1][o]);
-          const G4<T> zv1 = lds4(&Z1[b2 ^ 1][(zi + 2) * WU + 4 * (zg + 1)]);
-          const G4<T> zv2 = lds4(&Z2[b2 ^ 1][(zi + 1) * W2 + 4 * (zg + 2)]);
+          const G4<T> zv0 = tl_ld<WU>(Z0[sm1], orr, og);
+          const G4<T> zv1 = tl_ld<WU>(Z1[b2 ^ 1], zi + 2, zg + 1);
+          const G4<T> zv2 = tl_ld<W2>(Z2[b2 ^ 1], zi + 1, zg + 2);
           const bool own = i1z < v.n1 && gq >= 0 && gq < v.n0 && c_z < v.n2;
           G4<T> o0, o1, o2;
           T sdz = T(0), sz = T(0);

@@ -654,6 +654,48 @@ class PDS3DEngine:
                 break
         return self.result()
 
+    def time_parts(self, n):
+        """Mean duration (ms) of each launch of one single-GPU iteration over n eager iterations (HIP
+        events on the engine's stream): the in-plane normal operator (`nrm`), the axis-0 pass (`conv0`,
+        absent when it is folded into the update) and the update (`step`).  Leaves the loop state as
+        init_loop(n + 1, ...) set it; call init_loop again before a measured run."""
+        if self.world != 1:
+            raise ValueError('time_parts: single-GPU engines only')
+        L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), n + 1, n + 1, -1.0, 1, 2 * n + 6, L.stream()),
+                'pcs_ctrl_init2')
+        st = torch.cuda.current_stream()
+        ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        parts = {}
+        for i in range(n):
+            p = i % 2
+            marks = [('start', ev())]
+            marks[-1][1].record(st)
+            if self.fkind == L.PCS_F_GRADBUF and self.fused0 and self.ata:
+                nsub = self.rows + 2 * self.hx
+                self._ata_planes(L.ptr(self.X[p]), L.ptr(self.T[0]), nsub, L.stream())
+                marks.append(('nrm', ev()))
+                marks[-1][1].record(st)
+                if not self.fold:
+                    self._g_range(self.g_lo, min(self.hx + self.rows + 1, nsub), L.stream())
+                    marks.append(('conv0', ev()))
+                    marks[-1][1].record(st)
+            elif self.fkind == L.PCS_F_GRADBUF:
+                self._gradient(p, L.stream())
+                marks.append(('gradient', ev()))
+                marks[-1][1].record(st)
+            a = self.args[p]
+            a.hist = None
+            L.check(self.lib.pcs_pds3d_step(ctypes.byref(a), L.stream()), 'pcs_pds3d_step')
+            marks.append(('step', ev()))
+            marks[-1][1].record(st)
+            parts.setdefault(i, marks)
+        torch.cuda.synchronize()
+        out = {}
+        for marks in parts.values():
+            for (_, e0), (name, e1) in zip(marks[:-1], marks[1:]):
+                out.setdefault(name, []).append(e0.elapsed_time(e1))
+        return {k: float(np.mean(v)) for k, v in out.items()}
+
     def time_step_kernel(self, n):
         """Mean duration (ms) of pcs_pds3d_step alone over n eager launches (HIP events)."""
         st = torch.cuda.current_stream()

@@ -306,7 +306,7 @@ class SlabPDS2D:
     """
 
     def __init__(self, spec, dtype, tau, sigma, rho, x0, z0, rank, world, comm=None, chunk=16, native='auto',
-                 overlap=True):
+                 overlap=True, depth=1):
         self.lib = L.gpu()
         self.comm = comm
         self.rank, self.world = int(rank), int(world)
@@ -370,16 +370,36 @@ class SlabPDS2D:
         else:
             hx, hy = (1, 1) if fwd else (2, 2)
         hz = 1 if fwd else 4
+        # communication-avoiding depth (pcs_slab2d_deep_*): halos `depth` iterations deep, exchanged once per
+        # chunk of `depth` iterations; iteration j of a chunk also computes (depth - j) * reach rows of each
+        # halo, reach = the rows one iteration reads past its own (x and z), rounded up to even
+        self.depth = int(depth)
+        if not 1 <= self.depth <= L.DEEP_MAX:
+            raise ValueError(f'depth must be in 1..{L.DEEP_MAX}')
+        self.reach = 0
+        if self.depth > 1:
+            if mode not in ('pointwise', 'sep'):
+                raise ValueError(f'deep halos need the banded row-marching step (F mode {mode!r} has none)')
+            r = max(hx, hz)
+            self.reach = r + r % 2
+            e = (self.depth - 1) * self.reach
+            hx, hy, hz = hx + e, hy + e, hz + e
         if world > 1 and self.rows < max(hx, hy, hz):
             raise ValueError(f'slab of {self.rows} rows is thinner than its halo ({max(hx, hy, hz)} rows)')
         self.hx, self.hy, self.hz = hx, hy, hz
+        self.nbuf = max(2, self.depth)
         a.halo_x, a.halo_y, a.halo_z = hx, hy, hz
         N = n0 * n1
-        self.X = [lay.window(O.to_dev(x0, dtype), hx) for _ in range(2)]
+        # deep halos: the virtual slab of an iteration whose extension is clipped on one side moves each
+        # array's view by up to (depth - 1) reach / 2 rows (pcs_slab2d_deep_*), so the buffers carry that many
+        # zero rows of padding before and after their stored rows: the view's surplus loads stay in memory
+        self.pad = (self.depth - 1) * self.reach // 2
+        self.X = [self._padded(lay.window(O.to_dev(x0, dtype), hx)) for _ in range(self.nbuf)]
         z0d = O.to_dev(z0, dtype)
-        self.Z = [torch.cat([lay.window(z0d[c * N:(c + 1) * N], hz) for c in range(nc)]) for _ in range(2)]
+        self.Z = [self._padded(torch.cat([lay.window(z0d[c * N:(c + 1) * N], hz) for c in range(nc)]))
+                  for _ in range(self.nbuf)]
         if fk in (L.PCS_F_DENOISE, L.PCS_F_SEPCONV, L.PCS_F_CONV2D):
-            self.y = lay.window(-O.to_dev(spec['shift'], dtype), hy)  # y = -shift, exactly
+            self.y = self._padded(lay.window(-O.to_dev(spec['shift'], dtype), hy))  # y = -shift, exactly
             a.y = self.y.data_ptr()
         if mode in ('sep_normal', 'conv2d'):
             self.Gb = torch.zeros_like(self.X[0])  # grad F on the stored rows (x's layout)
@@ -398,7 +418,7 @@ class SlabPDS2D:
                 # (pds_nm64.hip, its N tables in fp64)
                 self.ntaps = torch.as_tensor(nmarch_taps(t0, t1, half, np.float64 if f64 else np.float32)).to(dev)
                 a.ntaps = self.ntaps.data_ptr()
-            self.cty = self._cty_window(spec, hy).to(dtype).contiguous()
+            self.cty = self._padded(self._cty_window(spec, hy).to(dtype).contiguous())
             a.cty = self.cty.data_ptr()
         self.nm_fused = False
         if mode in ('sep_normal', 'sep') and getattr(self, 'ntaps', None) is not None:
@@ -423,17 +443,29 @@ class SlabPDS2D:
         self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=dev)
         a.ctrl = self.ctrl.data_ptr()
-        self.args = [self._args_for(a, p) for p in (0, 1)]
-        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c) for c in range(nc)]) for q in (0, 1)]
+        self.args = [self._args_for(a, p) for p in range(self.nbuf)]
+        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c) for c in range(nc)])
+                      for q in range(self.nbuf)]
         self.hist = None
         self.chunk = max(1, int(chunk))
         # native loop (pcs_slab2d_run): one C call per chunk instead of five Python-issued
         # operations per iteration; needs an RCCL communicator when world > 1
-        if native == 'auto':
+        # native='local' (depth > 1, tests): the deep plan without a communicator, driven with the other ranks'
+        # plans of the same process by run_local_deep
+        self.local = native == 'local'
+        if self.local:
+            if self.depth < 2:
+                raise ValueError("native='local' is the deep-halo loop's in-process form (depth >= 2)")
+            native = True
+        elif native == 'auto':
             native = world == 1 or (comm is not None and comm.native() is not None)
         elif native and world > 1 and (comm is None or comm.native() is None):
             raise ValueError('native slab loop needs an RCCL (nccl backend) process group')
         self.native = bool(native)
+        if self.depth > 1 and not self.native:
+            raise ValueError('deep halos run in the native loop only (pcs_slab2d_deep_run): an RCCL process group')
+        self._deep = None
+        self._b = 0
         # the gradient passes of 'conv2d' / 'sep_normal' run once per iteration over the whole slab:
         # no banded (overlapped) schedule for them
         self.overlap = bool(overlap) and (mode in ('pointwise', 'sep') or self.nm_fused)
@@ -445,6 +477,16 @@ class SlabPDS2D:
         gc = int(os.environ.get('PCS_SLAB_GRAPH', '32' if world > 1 else '0') or 0)
         self.graph_chunk = (gc + gc % 2) if self.native and gc > 0 else 0
         self._graph = None
+
+    def _padded(self, t):
+        """t inside a buffer with self.pad zero rows before and after it (the view keeps the storage alive);
+        t itself when there is no padding."""
+        if self.pad == 0:
+            return t
+        p = self.pad * self.n1
+        buf = torch.zeros(t.numel() + 2 * p, dtype=t.dtype, device=t.device)
+        buf[p:p + t.numel()] = t
+        return buf[p:p + t.numel()]
 
     def _cty_window(self, spec, h):
         """Rows [row0 - h, row0 + rows + h) of Conv^T y (fp64, zeros outside the image), computed on
@@ -465,7 +507,7 @@ class SlabPDS2D:
         return out
 
     @classmethod
-    def from_pds(cls, pds, comm, rank=None, world=None, chunk=16, native='auto', overlap=True):
+    def from_pds(cls, pds, comm, rank=None, world=None, chunk=16, native='auto', overlap=True, depth=1):
         """This rank's slab of a PDS problem built with the public API on the global image
         (every rank builds the same problem, as a single-host script would)."""
         spec = pds._fused_spec()
@@ -474,13 +516,15 @@ class SlabPDS2D:
         rank = comm.rank if rank is None else rank
         world = comm.world if world is None else world
         return cls(spec, pds._compute_dtype(), pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank, world, comm, chunk,
-                   native, overlap)
+                   native, overlap, depth)
 
     def _args_for(self, a, p):
+        """The step from buffer set p to set p + 1 (mod nbuf; the ping-pong when nbuf == 2)."""
         b = L.PdsArgs()
         ctypes.pointer(b)[0] = a
-        b.x, b.xn = self.X[p].data_ptr(), self.X[1 - p].data_ptr()
-        b.z, b.zn = self.Z[p].data_ptr(), self.Z[1 - p].data_ptr()
+        q = (p + 1) % self.nbuf
+        b.x, b.xn = self.X[p].data_ptr(), self.X[q].data_ptr()
+        b.z, b.zn = self.Z[p].data_ptr(), self.Z[q].data_ptr()
         return b
 
     # ---- native loop
@@ -519,12 +563,38 @@ class SlabPDS2D:
         self._plan, self._plan_key = h, key
         return h
 
+    def _deep_plan(self):
+        """The communication-avoiding plan (pcs_slab2d_deep_create) of a depth > 1 slab."""
+        if self.hist is None:
+            self.hist = torch.full((2,), float('nan'), dtype=torch.float64, device=self.X[0].device)
+        key = (self.hist.data_ptr(),)
+        if self._deep is not None and self._deep_key == key:
+            return self._deep
+        self._destroy_plan()
+        d = L.SlabDeepDesc()
+        d.world, d.rank, d.depth, d.nbuf, d.reach = self.world, self.rank, self.depth, self.nbuf, self.reach
+        d.local = int(self.local)
+        for b in range(self.nbuf):
+            d.step[b] = self.args[b]
+            d.halo[b] = self._halo_set(b)
+        d.ctrl, d.hist = self.ctrl.data_ptr(), self.hist.data_ptr()
+        h = ctypes.c_void_p()
+        comm = self.comm.native() if self.world > 1 and not self.local else None
+        L.check(self.lib.pcs_slab2d_deep_create(ctypes.byref(d), comm, ctypes.byref(h)), 'pcs_slab2d_deep_create')
+        self._deep_desc = d
+        self._deep, self._deep_key = h, key
+        return h
+
     def _destroy_plan(self):
         self._graph = None  # captured against this plan's streams, events and buffers
         if self._plan is not None:
             torch.cuda.synchronize()
             L.load().pcs_slab2d_destroy(self._plan)
             self._plan = None
+        if getattr(self, '_deep', None) is not None:
+            torch.cuda.synchronize()
+            L.load().pcs_slab2d_deep_destroy(self._deep)
+            self._deep = None
 
     def overlapped(self):
         """True when the native loop overlaps the halo exchange with the interior band."""
@@ -588,10 +658,17 @@ class SlabPDS2D:
         L.check(self.lib.pcs_ctrl_init2(L.ptr(self.ctrl), int(min_iter), int(max_iter), float(accuracy_threshold),
                                         int(has_dual), int(self.hist.numel()), L.stream()), 'pcs_ctrl_init2')
         self._p = 0
+        self._b = 0
         return total
 
     def advance(self, k):
         """Enqueue k iterations (no host synchronisation, except the one-off schedule trial)."""
+        if self.depth > 1:  # chunks of `depth` iterations per halo exchange
+            if k:
+                L.check(self.lib.pcs_slab2d_deep_run(self._deep_plan(), int(k), self._b, L.stream()),
+                        'pcs_slab2d_deep_run')
+                self._b = (self._b + int(k)) % self.nbuf
+            return
         if self.native:
             if (not getattr(self, '_tuned', False) and self.world > 1 and self.overlap and k >= 8
                     and getattr(self.comm, 'tunable', False)):
@@ -680,7 +757,7 @@ class SlabPDS2D:
         """(n_iter, own rows of x, own rows of z (2 components), hist [n, 2])."""
         torch.cuda.synchronize()
         n = self.iterations()
-        q = n % 2
+        q = n % self.nbuf
         x = self.lay.rows_view(self.X[q], self.hx, 0, self.rows).clone()
         z = torch.cat([self.lay.rows_view(self.Z[q], self.hz, 0, self.rows, c) for c in range(self.ncomp)])
         h = self.hist[:2 * n].cpu().numpy().reshape(n, 2) if n > 0 else np.zeros((0, 2))
@@ -784,6 +861,31 @@ def run_local(slabs, max_iter, min_iter, accuracy_threshold, split=False):
                 for (_, recv), (send, _) in zip(lst, back):
                     recv.copy_(send)
         if (i + 1) % 8 == 0 and slabs[0].stopped():
+            break
+    return [s.result() for s in slabs]
+
+
+def run_local_deep(slabs, max_iter, min_iter, accuracy_threshold, chunk=None):
+    """All deep-halo slabs of one image inside one process through the native chunk loop with a
+    device-copy transport (pcs_slab2d_deep_run_local: the same launches, loop control and halo rows as
+    pcs_slab2d_deep_run, the all-gather and the exchange as copies); the host checks the stop flag
+    once per `chunk` iterations (default: 4 chunks of the depth)."""
+    slabs = sorted(slabs, key=lambda s: s.rank)
+    total = None
+    for s in slabs:
+        total = s.init_loop(max_iter, min_iter, accuracy_threshold)
+    lib = slabs[0].lib
+    plans = (ctypes.c_void_p * len(slabs))(*[s._deep_plan().value for s in slabs])
+    step = chunk or 4 * slabs[0].depth
+    done = 0
+    while done < total:
+        m = min(step, total - done)
+        L.check(lib.pcs_slab2d_deep_run_local(plans, len(slabs), m, slabs[0]._b, L.stream()),
+                'pcs_slab2d_deep_run_local')
+        for s in slabs:
+            s._b = (s._b + m) % s.nbuf
+        done += m
+        if slabs[0].stopped():
             break
     return [s.result() for s in slabs]
 

@@ -74,6 +74,11 @@ def test_self_launch_slab_headline_gloo_one_gpu():
     v = d['volume_c4']
     assert v['steps'] == 20 and v['it_per_s'] > 0, v
     assert v['halo_bytes_per_side_per_iter'] == v['comm']['halo_bytes_per_side'], v
+    # the metric as written: one --size^2 image split over the 2 ranks (strong scaling), beside the weak line
+    s = d['strong_4096']
+    assert s['scaling'] == 'strong' and s['it_per_s'] > 0 and s['steps'] == 6, s
+    assert s['depth'] == 1 and list(s['depth_trial_ms_per_iter']) == ['1'], s  # gloo: no RCCL, depth 1 only
+    assert s['comm']['exchange_ms'] > 0, s
 
 
 @pytest.mark.gpu

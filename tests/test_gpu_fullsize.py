@@ -160,3 +160,40 @@ def test_cps_fullsize_vs_oracle():
                                np.asarray(dr['primal'])[1:], rtol=1e-3)
     np.testing.assert_allclose(diag['Relative Improvement (dual variable)'].to_numpy(float)[1:],
                                np.asarray(dr['dual'])[1:], rtol=1e-3)
+
+
+@pytest.mark.parametrize('kind', ['forward', 'centered'])
+def test_c5_fullsize_fused_vs_generic(kind):
+    """C5 at its real size (BASELINE configs[4]: 1024^3 fp64, 15-tap Gaussian along every axis, 0.05 L21; the
+    reference's default centred K and the forward K): the fused 3-D engine (k_sep2d_nrmm + k_conv0_rta +
+    k_pds3d / k_pds3d_gen) against the operator-by-operator path for 3 iterations -- the only run of the
+    > 2^31-element indexing (z holds 3 * 1024^3 = 3.2e9 elements) outside the bench.  The oracle cannot run
+    at this size (its FFT convolution alone takes minutes per gradient); the generic path is the HIP
+    operators one call at a time, checked against the oracle at 48^3-128^3 elsewhere.  Bars: 1e-12 relative
+    on x and z (the two paths round the normal operator differently), finite, exact count, diagnostics 1e-9."""
+    import bench
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    n = 1024
+    out = []
+    for eng in ('fused', 'generic'):
+        pds = bench.build_volume(n, torch.float64, kind=kind)
+        pds.max_iter, pds.min_iter, pds.accuracy_threshold = NITER - 1, NITER - 1, 0.0
+        pds.engine_mode = eng
+        est, _, diag = pds.iterate()
+        assert pds.iter == NITER
+        if eng == 'fused':
+            assert isinstance(pds._engine, PDS3DEngine)
+        else:
+            assert pds._engine is None
+        out.append((est['primal_variable'], est['dual_variable'],
+                    diag['Relative Improvement (primal variable)'].to_numpy(float),
+                    diag['Relative Improvement (dual variable)'].to_numpy(float)))
+        del pds, est
+        torch.cuda.empty_cache()
+    assert out[0][1].numel() == 3 * n ** 3
+    for k in range(2):
+        assert torch.isfinite(out[0][k]).all()
+        d = float(torch.linalg.vector_norm(out[0][k] - out[1][k]) / torch.linalg.vector_norm(out[1][k]))
+        assert d < 1e-12, (k, d)
+    for k in (2, 3):
+        np.testing.assert_allclose(out[0][k][1:], out[1][k][1:], rtol=1e-9)

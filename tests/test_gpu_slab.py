@@ -474,6 +474,49 @@ def test_slab3d_banded_bitwise(world, n0, dtype):
     assert np.allclose(res[0][3][fin], h1[fin], rtol=1e-12 if dtype == np.float64 else 1e-5)
 
 
+@pytest.mark.parametrize('world,dtype,n0', [(4, np.float32, 124), (4, np.float32, 160),
+                                             (8, np.float64, 264), (8, np.float64, 320)])
+@pytest.mark.parametrize('kind', ['forward', 'centered'])
+def test_slab3d_many_ranks_bitwise(world, dtype, n0, kind):
+    """The rank counts BASELINE names (C4 on 4 GPUs in fp32, C5 on 8 in fp64), in one
+    process: slabs of 31 planes (2 x the 15-plane x halo + 1: the serial schedule, too thin for the bands) and
+    of 33 / 40 planes (the banded schedule, boundary bands of hx + 1 = 16 planes), forward and the default
+    centred K, every schedule -- serial, and the banded 'split' and 'fullg' orders -- bitwise equal to the
+    single-GPU engine, with the reference's iteration count."""
+    from pycsou_amd.opt.engine3d import PDS3DEngine
+    from pycsou_amd.parallel import run_local
+    pds = build(vol3d_case(n0, kind=kind), dtype, engine='fused')
+    spec = pds._fused_spec()
+    dt = pds._compute_dtype()
+    one = PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    n1, x1, z1, h1 = one.run(pds.max_iter, pds.min_iter, pds.accuracy_threshold)
+    assert n1 == 8
+    ran = []
+    for order in ('serial', 'split', 'fullg'):
+        slabs = [PDS3DEngine(spec, dt, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, rank=r, world=world)
+                 for r in range(world)]
+        rows = [s.rows for s in slabs]
+        assert sum(rows) == n0 and min(rows) >= 2 * slabs[0].hx + 1, rows
+        banded = all(s.banded for s in slabs)
+        assert banded == (min(rows) > 2 * slabs[0].band), (rows, banded)
+        if order != 'serial':
+            if not banded:
+                continue
+            for s in slabs:
+                s.order = order
+        res = run_local(slabs, pds.max_iter, pds.min_iter, pds.accuracy_threshold, split=order != 'serial')
+        assert all(r[0] == n1 for r in res)
+        x2 = torch.cat([r[1] for r in res])
+        z2 = torch.cat([torch.cat([r[2].view(3, -1)[c] for r in res]) for c in range(3)])
+        assert torch.equal(x2, x1), (order, (x2 - x1).abs().max().item())
+        assert torch.equal(z2, z1), (order, (z2 - z1).abs().max().item())
+        fin = np.isfinite(h1)
+        assert np.allclose(res[0][3][fin], h1[fin], rtol=1e-12 if dtype == np.float64 else 1e-5)
+        ran.append(order)
+        del slabs, res
+    assert ran == (['serial', 'split', 'fullg'] if n0 // world > 32 else ['serial'])
+
+
 def test_slab3d_two_process_overlap(tmp_path):
     """Two ranks (gloo, one GPU): the overlapped 3-D iteration (exchange started after the
     boundary bands, all-gather + loop control drained at the next iteration) against one GPU."""
@@ -634,3 +677,64 @@ def test_pds3d_advance_issues_exactly_k(k):
     eng.advance(k)
     torch.cuda.synchronize()
     assert eng.iterations() == 3 + k
+
+
+def _stop_threshold(pds, kind, niter, j):
+    """A primal relative-improvement threshold under which the single-GPU run stops after iteration j of
+    a `niter` fixed run (between the metric of iterations j - 1 and j)."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    spec = pds._fused_spec()
+    eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+    _, _, _, h = eng.run(niter - 1, niter - 1, 0.0)
+    m = h[:, 0]
+    assert np.all(m[:j] > m[j]), m[:j + 1]  # the first iteration whose metric falls below the threshold
+    return float(0.5 * (min(m[:j]) + m[j]))
+
+
+@pytest.mark.parametrize('kind,world,depth', [('deconv', 2, 2), ('deconv', 3, 4), ('deconv', 8, 4),
+                                              ('denoise', 3, 4), ('denoise', 5, 8)])
+def test_deep_halo_slabs_bitwise(kind, world, depth):
+    """The communication-avoiding slab loop (pcs_slab2d_deep_*: halos `depth` iterations deep, exchanged once
+    per chunk; each iteration also computes the shrinking redundant halo rows) in one process with the
+    device-copy transport: x, z bitwise the single-GPU engine and the same iteration count, for a fixed
+    count that ends mid-chunk and for a natural stop landing inside a chunk."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.parallel import SlabPDS2D, run_local_deep
+    pds = _problem(kind)
+    spec = pds._fused_spec()
+    thr = _stop_threshold(pds, kind, 40, 2 * depth)
+    for max_iter, min_iter, acc in ((21, 21, 0.0), (200, 2, thr)):
+        eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+        n, x1, z1, h1 = eng.run(max_iter, min_iter, acc)
+        if acc > 0:
+            assert n == 2 * depth + 1, (n, depth)  # the stop lands inside a chunk
+        slabs = [SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, r, world,
+                           native='local', depth=depth) for r in range(world)]
+        assert all(s.depth == depth and s.nbuf == max(2, depth) for s in slabs)
+        res = run_local_deep(slabs, max_iter, min_iter, acc, chunk=depth)
+        assert all(r[0] == n for r in res), ([r[0] for r in res], n)
+        x2 = torch.cat([r[1] for r in res])
+        z2 = torch.cat([torch.cat([r[2][:r[2].numel() // 2] for r in res]),
+                        torch.cat([r[2][r[2].numel() // 2:] for r in res])])
+        assert torch.equal(x2, x1), (x2 - x1).abs().max().item()
+        assert torch.equal(z2, z1), (z2 - z1).abs().max().item()
+        assert np.allclose(res[0][3][1:], h1[1:], rtol=1e-5)
+
+
+def test_deep_halo_world1_native_run():
+    """depth > 1 on one rank (no neighbours: no redundant rows, the loop control once per chunk): the
+    native pcs_slab2d_deep_run loop against the single-GPU engine, fixed count and natural stop."""
+    from pycsou_amd.opt.engine import PDS2DEngine
+    from pycsou_amd.parallel import SlabPDS2D
+    pds = _problem('deconv')
+    spec = pds._fused_spec()
+    thr = _stop_threshold(pds, 'deconv', 40, 10)
+    for max_iter, min_iter, acc in ((21, 21, 0.0), (200, 2, thr)):
+        eng = PDS2DEngine(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0)
+        n, x1, z1, h1 = eng.run(max_iter, min_iter, acc)
+        s = SlabPDS2D(spec, torch.float32, pds.tau, pds.sigma, pds.rho, pds.x0, pds.z0, 0, 1, native=True, depth=4,
+                      chunk=8)
+        n2, x2, z2, h2 = s.run(max_iter, min_iter, acc)
+        assert n2 == n
+        assert torch.equal(x2, x1) and torch.equal(z2, z1)
+        assert np.allclose(h2[1:], h1[1:], rtol=1e-5)
