@@ -469,7 +469,9 @@ int pcs_pds_finalize_pending(const double* part, int64_t np, void* ctrl, double*
 
 int pcs_pds_reduce_finalize_k(const double* gathered, int world, int k, void* ctrl, double* hist, hipStream_t st) {
   if (!gathered || !ctrl || !hist || world < 1 || world > kRedThreads || k < 1) return PCS_EINVAL;
-  k_reduce_finalize_k<<<1, kRedThreads, 0, st>>>(gathered, world, k, (Ctrl*)ctrl, hist);
+  // one wave when the ranks fit in it: the same sums as the 1024-thread tree (the other waves add zeros),
+  // a fraction of its barriers per iteration
+  k_reduce_finalize_k<<<1, world <= 64 ? 64 : kRedThreads, 0, st>>>(gathered, world, k, (Ctrl*)ctrl, hist);
   return launch_status();
 }
 

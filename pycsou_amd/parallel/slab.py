@@ -376,12 +376,11 @@ class SlabPDS2D:
         self.depth = int(depth)
         if not 1 <= self.depth <= L.DEEP_MAX:
             raise ValueError(f'depth must be in 1..{L.DEEP_MAX}')
-        self.reach = 0
+        r = max(hx, hz)
+        self.reach = r + r % 2
         if self.depth > 1:
             if mode not in ('pointwise', 'sep'):
                 raise ValueError(f'deep halos need the banded row-marching step (F mode {mode!r} has none)')
-            r = max(hx, hz)
-            self.reach = r + r % 2
             e = (self.depth - 1) * self.reach
             hx, hy, hz = hx + e, hy + e, hz + e
         if world > 1 and self.rows < max(hx, hy, hz):
@@ -454,8 +453,6 @@ class SlabPDS2D:
         # plans of the same process by run_local_deep
         self.local = native == 'local'
         if self.local:
-            if self.depth < 2:
-                raise ValueError("native='local' is the deep-halo loop's in-process form (depth >= 2)")
             native = True
         elif native == 'auto':
             native = world == 1 or (comm is not None and comm.native() is not None)
@@ -663,7 +660,7 @@ class SlabPDS2D:
 
     def advance(self, k):
         """Enqueue k iterations (no host synchronisation, except the one-off schedule trial)."""
-        if self.depth > 1:  # chunks of `depth` iterations per halo exchange
+        if self.depth > 1 or self.local:  # chunks of `depth` iterations per halo exchange
             if k:
                 L.check(self.lib.pcs_slab2d_deep_run(self._deep_plan(), int(k), self._b, L.stream()),
                         'pcs_slab2d_deep_run')
