@@ -274,8 +274,17 @@ class PDS3DEngine:
         self.args = [self._args_for(p) for p in (0, 1)]
         self.sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self.gathered = torch.zeros(4 * world, dtype=torch.float64, device=dev)
-        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c) for c in range(3)])
+        # z halo planes the update reads (the exchange moved every component's full halo).
+        # Backward / centred K: K^T z at plane p reads z0 of p - 1 .. p + 1 and the segments' one-plane-early
+        # start / one-past end read z0 two planes out but z1 / z2 of one halo plane only (they are in-plane
+        # derivatives): z1 / z2 send 1 of their 2 stored planes (C5/8: 19 planes per side instead of 21).
+        # Forward K reads z0 one plane below and above, z1 / z2 one plane above (u on the plane past the slab),
+        # all of its 1-plane halos (a one-directional z1 / z2 exchange would shorten the upward messages only,
+        # and the downward ones, which carry them, set the exchange time)
+        self.zdepth = (1, 1, 1) if self.kkind == L.PCS_FORWARD else (2, 1, 1)
+        self.halos = [lay.halo_pairs([(self.X[q], hx, 0)] + [(self.Z[q], hz, c, self.zdepth[c]) for c in range(3)])
                       for q in (0, 1)] if world > 1 else [{}, {}]
+        self.halo_planes = hx + sum(self.zdepth)  # planes one side sends per iteration
         self.hist = None
         self.graph = None
         self.chunk = max(2, chunk + chunk % 2)

@@ -284,16 +284,19 @@ class SlabLayout:
         return buf[base + (r0 + h) * n1: base + (r1 + h) * n1]
 
     def halo_pairs(self, bufs):
-        """bufs: [(buffer, h, comp), ...] -> {peer: [(send, recv), ...]}: own boundary rows go
-        to the neighbour's halo, the neighbour's boundary rows fill ours."""
+        """bufs: [(buffer, h, comp[, d]), ...] -> {peer: [(send, recv), ...]}: own boundary rows go
+        to the neighbour's halo, the neighbour's boundary rows fill ours -- the d <= h rows next to the
+        own rows (default all h stored rows; d = 0 leaves the buffer out of the exchange)."""
         pairs = {}
         R = self.rows
+        full = [(b[0], b[1], b[2], b[3] if len(b) > 3 else b[1]) for b in bufs]
+        full = [(b, h, c, d) for b, h, c, d in full if d > 0]
         if self.rank > 0:
-            pairs[self.rank - 1] = [(self.rows_view(b, h, 0, h, c), self.rows_view(b, h, -h, 0, c))
-                                    for b, h, c in bufs]
+            pairs[self.rank - 1] = [(self.rows_view(b, h, 0, d, c), self.rows_view(b, h, -d, 0, c))
+                                    for b, h, c, d in full]
         if self.rank < self.world - 1:
-            pairs[self.rank + 1] = [(self.rows_view(b, h, R - h, R, c), self.rows_view(b, h, R, R + h, c))
-                                    for b, h, c in bufs]
+            pairs[self.rank + 1] = [(self.rows_view(b, h, R - d, R, c), self.rows_view(b, h, R, R + d, c))
+                                    for b, h, c, d in full]
         return pairs
 
 

@@ -23,6 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from pycsou_amd import _lib as L  # noqa: E402
+
 
 def build(n, dtype, seed=0, kind='forward'):
     from pycsou_amd.func.loss import SquaredL2Loss
@@ -69,6 +71,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=4)
     ap.add_argument('--rank-of', type=int, default=0)
     ap.add_argument('--kind', default='forward', choices=['forward', 'backward', 'centered'])
+    ap.add_argument('--one-gpu-ms', type=float, default=0.0,
+                    help='--rank-of: the single-GPU ms per iteration of the same volume (the link-rate model '
+                         'prints the speed-up it implies)')
     args = ap.parse_args()
     if args.rank_of > 1:
         return rank_share(args)
@@ -146,7 +151,7 @@ def rank_share(args):
     rank = W // 2 - 1 if W > 2 else 0
     t0 = time.time()
     print(f'building {args.size}^3 ...', flush=True)
-    pds = build(args.size, dtype)
+    pds = build(args.size, dtype, kind=args.kind)
     spec = pds._fused_spec()
     print(f'built in {time.time() - t0:.1f} s', flush=True)
     K = -(-args.steps // 8) * 8  # whole chunks of 8 (the graph variants replay chunks)
@@ -172,9 +177,54 @@ def rank_share(args):
         out['planes'], out['banded'] = eng.rows, bool(eng.banded)
         print(name, out[f'{name}_ms_per_iter'], 'ms/iter', flush=True)
         esz = eng.X[0].element_size()
-        out['halo_bytes_per_side'] = (eng.hx + 3 * eng.hz) * eng.plane * esz
+        out['halo_bytes_per_side'] = eng.halo_planes * eng.plane * esz
+        if ov and not graph and eng.banded:
+            # the overlap window of this order: the exchange starts after the boundary bands and is awaited
+            # after the next iteration's in-plane pass of the own planes -> window = interior + that pass
+            ph = {'pre': [], 'boundary': [], 'interior': []}
+            st = torch.cuda.current_stream()
+            for i in range(4):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                ev[0].record(st)
+                eng._band_pre(i % 2, L.stream())
+                ev[1].record(st)
+                eng._band_boundary(i % 2, L.stream())
+                ev[2].record(st)
+                eng._band_interior(i % 2, L.stream())
+                ev[3].record(st)
+                torch.cuda.synchronize()
+                for k, (a, b) in zip(ph, zip(ev[:-1], ev[1:])):
+                    ph[k].append(a.elapsed_time(b))
+            ph = {k: float(np.median(v)) for k, v in ph.items()}
+            out[f'{name}_phases_ms'] = {k: round(v, 4) for k, v in ph.items()}
+            out[f'{name}_window_ms'] = round(ph['interior'] + ph['pre'], 4)
         del eng
         torch.cuda.empty_cache()
+    # link-rate model: per direction and neighbour, the exchange takes halo / R; the banded
+    # orders hide it behind their window, the serial schedule adds it.  Iteration = compute + exposed exchange
+    hb = out['halo_bytes_per_side']
+    model = {}
+    for gbs in (50.0, 82.0, 120.0, 153.0):
+        tx = hb / (gbs * 1e9) * 1e3
+        est = {'serial': out['serial_ms_per_iter'] + tx}
+        for name in ('banded', 'banded_fullg'):
+            if f'{name}_window_ms' in out:
+                est[name] = out[f'{name}_ms_per_iter'] + max(0.0, tx - out[f'{name}_window_ms'])
+        best = min(est, key=est.get)
+        m = {'exchange_ms': round(tx, 3), 'best_order': best, 'iteration_ms': round(est[best], 3)}
+        if args.one_gpu_ms > 0:
+            m['speedup'] = round(args.one_gpu_ms / est[best], 2)
+        model[f'{gbs:.0f}GBps'] = m
+    out['link_model'] = model
+    if args.one_gpu_ms > 0:
+        # the slowest link at which W GPUs still reach 6x: exchange <= T1 / 6 - compute + window, best order
+        rates = {}
+        for name in ('banded', 'banded_fullg'):
+            if f'{name}_window_ms' in out:
+                slack = args.one_gpu_ms / 6 - out[f'{name}_ms_per_iter'] + out[f'{name}_window_ms']
+                if slack > 0:
+                    rates[name] = round(hb / (slack * 1e-3) / 1e9, 1)
+        out['min_GBps_for_6x'] = rates
     print(json.dumps(out), flush=True)
 
 
