@@ -17,7 +17,9 @@ def per_launch(path, counter, kern):
             if r['Counter_Name'] == counter and kern in r['Kernel_Name']]
     if not vals:
         raise SystemExit(f'no {counter} rows for {kern} in {path}')
-    return sum(vals) / len(vals), len(vals)
+    # launches that found the loop already stopped move (almost) nothing: average the working ones
+    work = [v for v in vals if v >= 0.5 * max(vals)]
+    return sum(work) / len(work), len(work)
 
 
 def main():
