@@ -299,7 +299,7 @@ def volume_bench(n, dtype, K, W, world, rank, kind='forward'):
                     'words_per_voxel_iteration': sum(words[k] for k in per),
                     'source': 'HIP-event pairs around each launch of 3 eager iterations after the timed region'}
     alg = 9 * n ** 3 * elem  # (2d+3) N words, d = 3: read x, z (3N), y; write x', z' (3N)
-    halo = 0 if world == 1 else (eng.hx + 3 * eng.hz) * eng.plane * elem
+    halo = 0 if world == 1 else eng.halo_planes * eng.plane * elem
     res = {'workload': f'{"C5" if elem == 8 else "C4"} 3-D TV-deconvolution {n}^3 {"f64" if elem == 8 else "f32"}, 15-tap Gaussian per axis '
                        f'(Convolve1D x3), 3-D Gradient(kind={kind}), 0.05*L21Norm, PDS3DEngine '
                        f'({"k_pds3d" if kind == "forward" else "k_pds3d_gen"} update), '
