@@ -581,15 +581,18 @@ __global__ __launch_bounds__(NrmF::NT, 3) void k_sep2d_nrm(const T* __restrict__
       // 4-row chunks: 0.543 against 0.565-0.573 ms for 8 (512^3 fp32, profiles/r2_nrm_ablation.txt)
       constexpr int NV = RB + 28, CH = 4, NCH = (NV + CH - 1) / CH;
       const T* rcol = ring + 4 * vg;
+      // window row v sits at ring slot base + v, wrapped once at most: two bases (the second one ring
+      // length back) and a per-row select, the row offset an immediate of the LDS read -- instead of
+      // recomputing the wrapped slot and its address for every row (round 6)
+      const T* rb0 = rcol + base * TP;
+      const T* rb1 = rb0 - RING * TP;
+      const int wrap = RING - base;  // the first window row past the ring's end
       Q4<T> w[2][CH];  // chunk c in w[c & 1] (static after unrolling: no register copies)
       auto rd = [&](int c, Q4<T>(&wc)[CH]) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-          if (c * CH + j < NV) {
-            int slot = base + c * CH + j;
-            slot = slot >= RING ? slot - RING : slot;
-            wc[j] = ldsq(rcol + slot * TP);
-          }
+          const int v = c * CH + j;
+          if (v < NV) wc[j] = ldsq((v < wrap ? rb0 : rb1) + v * TP);
         }
       };
       rd(0, w[0]);
