@@ -663,6 +663,49 @@ def leg_cps_inpaint(args, dtype, K, W):
                          'unit': 'GB/s', 'frac': round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
+def _timed_iters(eng, iters, native):
+    """ms per iteration of `iters` iterations through the real transport, max over ranks."""
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    eng.advance(iters)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device='cuda' if native else 'cpu')
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()) * 1e3 / iters
+
+
+def depth_trial(pds, comm, eng1, depths, W, K):
+    """The communication-avoiding depth of a multi-rank slab run (native RCCL loop): the depth-1 engine
+    `eng1` (its serial / overlapped schedule trial included) and one deep-halo engine per depth in `depths`
+    each run 16 untimed then 32 timed iterations through the real transport; the fastest (max over ranks)
+    is returned with the trial times.  A depth whose halo does not fit the slabs is skipped."""
+    from pycsou_amd.parallel import SlabPDS2D
+    trials, best, best_ms = {}, None, None
+    for d in (1,) + tuple(depths):
+        if d == 1:
+            eng = eng1
+        else:
+            try:
+                eng = SlabPDS2D.from_pds(pds, comm, native=True, depth=d)
+            except ValueError as e:  # a slab thinner than the deep halo: that depth does not apply
+                trials[d] = f'skipped: {e}'[:120]
+                continue
+        total = 64 + W + K
+        eng.init_loop(total, total, -1.0)
+        eng.advance(16)  # untimed (plan creation; depth 1: its schedule trial)
+        ms = _timed_iters(eng, 32, True)
+        trials[d] = round(ms, 4)
+        if best_ms is None or ms < best_ms:
+            if best is not None and best is not eng1:
+                best._destroy_plan()
+            best, best_ms = eng, ms
+        elif eng is not eng1:
+            eng._destroy_plan()
+    return best, trials
+
+
 def slab_bench(n, dtype, K, W, world):
     """Weak scaling: a (n world) x n image, one n x n row slab per rank; K timed iterations
     (barrier + synchronize on both sides; the caller takes the max over ranks)."""
@@ -686,12 +729,17 @@ def slab_bench(n, dtype, K, W, world):
                   f'torch.distributed per-iteration loop (reported as loop_fallback=true)', file=sys.stderr)
             eng = SlabPDS2D.from_pds(pds, comm, native=False, **kw)
             fallback = True
+    trials = None
+    if world > 1 and eng.native:
+        # communication-avoiding depths (halos k iterations deep, one exchange per k iterations): kept only when
+        # faster through the real transport than the per-iteration exchange
+        eng, trials = depth_trial(pds, comm, eng, (2, 4), W, K)
     del pds
     torch.cuda.empty_cache()
     total = W + K + 4
     eng.init_loop(total, total, -1.0)
     spin_up(eng, min(K, 50))
-    if world > 1:  # the one-off serial / overlapped schedule trial runs here, never in the timed region
+    if world > 1 and eng.depth == 1:  # the one-off serial / overlapped schedule trial, never in the timed region
         eng.init_loop(total, total, -1.0)
         eng.advance(8)
         torch.cuda.synchronize()
@@ -716,11 +764,14 @@ def slab_bench(n, dtype, K, W, world):
         dt = float(t.item())
     probe = comm_probe(eng) if world > 1 else None  # compute / all-gather / exchange timed apart
     kern_ms = eng.time_step_kernel(min(K, 100))  # a step here also holds the sums all-gather + halos
-    loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else (
-        'python (gloo rehearsal)' if world > 1 and dist.get_backend() != 'nccl' else 'python')
+    if eng.depth > 1:
+        loop = f'native deep-halo, depth {eng.depth} (pcs_slab2d_deep_run)'
+    else:
+        loop = ('native, overlapped halo exchange' if eng.overlapped() else 'native, serial') if eng.native else (
+            'python (gloo rehearsal)' if world > 1 and dist.get_backend() != 'nccl' else 'python')
     return {'ms_per_step': dt * 1e3 / K, 'kernel_ms': kern_ms, 'kernel_ms_isolated': kern_ms, 'nblocks': eng.nblocks,
             'loop': loop, 'loop_fallback': fallback, 'schedule_trial_ms': getattr(eng, 'tune_ms', None),
-            'comm': probe}
+            'depth': eng.depth, 'depth_trial_ms_per_iter': trials, 'comm': probe}
 
 
 def strong_bench(n, dtype, K, W, world, depths=(1, 2, 4, 8)):
@@ -738,44 +789,16 @@ def strong_bench(n, dtype, K, W, world, depths=(1, 2, 4, 8)):
     native = dist.get_backend() == 'nccl'
     rank = comm.rank
     rows = row_split(n, world, rank)[1]
-    trials, best, best_ms = {}, None, None
-
-    def timed(eng, iters):
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        eng.advance(iters)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device='cuda' if native else 'cpu')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()) * 1e3 / iters
-
-    for d in (depths if native else (1,)):
-        try:
-            eng = SlabPDS2D.from_pds(pds, comm, native=native, depth=d)
-        except ValueError as e:  # a slab thinner than the deep halo: that depth does not apply
-            trials[d] = f'skipped: {e}'[:120]
-            continue
-        if d == 1 and native:
-            eng.overlapped()
-        total = 64 + W + K
-        eng.init_loop(total, total, -1.0)
-        eng.advance(16)  # untimed (plan creation; depth 1: its schedule trial)
-        ms = timed(eng, 32)
-        trials[d] = round(ms, 4)
-        if best_ms is None or ms < best_ms:
-            if best is not None:
-                best._destroy_plan()
-            best, best_ms = eng, ms
-        else:
-            eng._destroy_plan()
-            del eng
-    eng = best
+    eng = SlabPDS2D.from_pds(pds, comm, native=native, depth=1)
+    if native:
+        eng.overlapped()
+        eng, trials = depth_trial(pds, comm, eng, tuple(d for d in depths if d > 1), W, K)
+    else:
+        trials = {1: None}
     total = W + K + 4
     eng.init_loop(total, total, -1.0)
     eng.advance(W)
-    ms = timed(eng, K)
+    ms = _timed_iters(eng, K, native)
     assert eng.iterations() == W + K, (eng.iterations(), W, K)
     probe = comm_probe(eng)
     elem = 4 if dtype == torch.float32 else 8
@@ -793,7 +816,7 @@ def strong_bench(n, dtype, K, W, world, depths=(1, 2, 4, 8)):
     if probe is not None and eng.depth > 1:
         probe['per'] = f'one chunk of {eng.depth} iterations (all-gather of {4 * eng.depth} sums, deep-halo exchange)'
     eng._destroy_plan()
-    del eng, best, pds
+    del eng, pds
     comm.close()
     torch.cuda.empty_cache()
     return res
