@@ -555,13 +555,17 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
 // volume.  Traffic per voxel: x, g, z (3) in; x', z' (3) out = 9 words (the forward kernel's),
 // plus the tile halos (rows +- 1, one 4-group per side).
 // Tile rows: 16 for fp32 (vertical halo 2/16: PMC reads 1.39x -> ~1.24x the algorithmic at 8 rows;
-// 101 KB of LDS), 8 for fp64 (the 16-row rings would need 202 KB)
+// 101 KB of LDS), 12 for fp64 (155.5 KB; 16 rows would need 202 KB.  C5 centred: 17.1 ms against 18.4 at
+// 8 rows, reads 1.45x -> ~1.33x the algorithmic; 10 rows measured 20.0 ms, profiles/r6_g64rows_ab.txt)
 constexpr int k3gTW = 128, k3gNT = 512;
 #ifndef PCS_3DG_ROWS32  // fp32 tile rows (diagnostics builds override)
 #define PCS_3DG_ROWS32 16
 #endif
+#ifndef PCS_3DG_ROWS64  // fp64 tile rows (diagnostics builds override)
+#define PCS_3DG_ROWS64 12
+#endif
 template <typename T>
-constexpr int k3g_rows() { return sizeof(T) == 4 ? PCS_3DG_ROWS32 : 8; }
+constexpr int k3g_rows() { return sizeof(T) == 4 ? PCS_3DG_ROWS32 : PCS_3DG_ROWS64; }
 
 #ifndef PCS_3DG_MINB  // workgroups per CU the register budget targets (diagnostics builds override)
 #define PCS_3DG_MINB 1
@@ -874,11 +878,22 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
     (void)hipGetLastError();
     return (int64_t)cus;  // one 512-thread workgroup per CU
   }();
-  int64_t nseg = (target + per_plane - 1) / per_plane;
+  // the segment count minimises the makespan: (rounds of `target` workgroups) x (segment length + the
+  // two-plane prologue).  A plane of tiles that is not a multiple of the CU count otherwise leaves a
+  // partial last round: C5 at 12-row fp64 tiles is 688 tiles per plane = 2.69 rounds of 1024 planes run
+  // as 3; 7 segments of 147 planes run 19 rounds of 147 (2793 plane-times against 3072)
   const int64_t max_seg = (L + 7) / 8;
-  nseg = nseg > max_seg ? max_seg : nseg;
-  nseg = nseg < bands ? bands : nseg;
-  nseg = nseg < 1 ? 1 : nseg;
+  int64_t lo = (target + per_plane - 1) / per_plane;
+  lo = lo > max_seg ? max_seg : lo;
+  lo = lo < bands ? bands : lo;
+  lo = lo < 1 ? 1 : lo;
+  int64_t nseg = lo, best = -1;
+  for (int64_t ns = lo; ns <= max_seg && ns <= lo + 15; ++ns) {
+    const int64_t sl = (L + ns - 1) / ns;
+    const int64_t tasks = per_plane * ((L0 + sl - 1) / sl + (L1 + sl - 1) / sl);
+    const int64_t cost = (tasks + target - 1) / target * (sl + 2);
+    if (best < 0 || cost < best) best = cost, nseg = ns;
+  }
   const int64_t seg_len = (L + nseg - 1) / nseg;
   const int64_t n0 = seg_len ? (L0 + seg_len - 1) / seg_len : 0, n1 = seg_len ? (L1 + seg_len - 1) / seg_len : 0;
   p.bd = Bands{(int)seg_len, (int)n0, (int)pb.a0, (int)pb.b0, (int)pb.a1, (int)pb.b1};
