@@ -160,6 +160,13 @@ __device__ __forceinline__ void tl_st(double* a, int r, int g, const G4<double>&
 // 8 x 128 tiles: a 64-column tile's one-group right halo costs a third 128-B line per row
 // (PMC: 1.53x the algorithmic reads); at 128 columns it is one line in five
 constexpr int k3T1 = 8, k3TW = PCS_K3TW;
+// fp64 forward-K tile rows (diagnostics builds override): 12 (113.5 KB of LDS, one 512-thread workgroup per
+// CU as at 8) -- C5 update 13.83 against 14.22 ms at 8 (profiles/r6_f3rows_ab.txt)
+#ifndef PCS_3D_ROWS64
+#define PCS_3D_ROWS64 12
+#endif
+template <typename T>
+constexpr int k3_rows() { return sizeof(T) == 8 ? PCS_3D_ROWS64 : k3T1; }
 // fp64 forward-K tile width (diagnostics builds override): 64 columns = 256-thread workgroups, three of
 // them per CU at the fp64 kernel's 157-169 VGPRs instead of one 512-thread one -- measured slower (C5
 // update 17.0 against 14.9 ms, profiles/r4_c5_tile64_ab.txt): 128 stays
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
                                                  int off0) {
   // PCS_F_CONV0: a second set of k3NT threads (waves 8-15) runs the axis-0 rings beside the update
   constexpr bool FOLD = FK == PCS_F_CONV0;
-  constexpr int T1 = k3T1, TW = K3<T>::TW, NT = FOLD ? 2 * K3<T>::NT : K3<T>::NT;
+  constexpr int T1 = k3_rows<T>(), TW = K3<T>::TW, NT = FOLD ? 2 * K3<T>::NT : K3<T>::NT;
   constexpr int UR = T1 + 1, WG = TW + 4, GG = WG / 4;
   constexpr int NU = UR * GG;                 // U items (x_t / u), 153
   constexpr int NZ = T1 * (TW / 4);           // z' items, 128
@@ -850,7 +857,7 @@ struct PlaneBands {
 // update-tile rows of the launch: the forward kernel's 8, or the general-K kernel's (k3g_rows)
 static int tile_rows3(const pcs_pds3d_args* a) {
   if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) return a->dtype == PCS_F32 ? k3g_rows<float>() : k3g_rows<double>();
-  return k3T1;
+  return a->dtype == PCS_F32 ? k3_rows<float>() : k3_rows<double>();
 }
 
 static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
