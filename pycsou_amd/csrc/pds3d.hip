@@ -564,7 +564,17 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
 // Tile rows: 16 for fp32 (vertical halo 2/16: PMC reads 1.39x -> ~1.24x the algorithmic at 8 rows;
 // 101 KB of LDS), 12 for fp64 (155.5 KB; 16 rows would need 202 KB.  C5 centred: 17.1 ms against 18.4 at
 // 8 rows, reads 1.45x -> ~1.33x the algorithmic; 10 rows measured 20.0 ms, profiles/r6_g64rows_ab.txt)
-constexpr int k3gTW = 128, k3gNT = 512;
+#ifndef PCS_3DG_NT32  // fp32 workgroup size (diagnostics builds override)
+#define PCS_3DG_NT32 512
+#endif
+constexpr int k3gTW = 128;
+template <typename T>
+constexpr int k3g_nt() { return sizeof(T) == 4 ? PCS_3DG_NT32 : 512; }
+#ifndef PCS_3DG_SETS32  // fp32 prefetch register sets (diagnostics builds override)
+#define PCS_3DG_SETS32 2
+#endif
+template <typename T>
+constexpr int k3g_sets() { return sizeof(T) == 4 ? PCS_3DG_SETS32 : 2; }
 #ifndef PCS_3DG_ROWS32  // fp32 tile rows (diagnostics builds override)
 #define PCS_3DG_ROWS32 16
 #endif
@@ -574,16 +584,19 @@ constexpr int k3gTW = 128, k3gNT = 512;
 template <typename T>
 constexpr int k3g_rows() { return sizeof(T) == 4 ? PCS_3DG_ROWS32 : PCS_3DG_ROWS64; }
 
+#ifndef PCS_3DG_ROWFORM  // column-border tiles with the row axis interior get their own code form (A/B knob)
+#define PCS_3DG_ROWFORM 1
+#endif
 #ifndef PCS_3DG_MINB  // workgroups per CU the register budget targets (diagnostics builds override)
 #define PCS_3DG_MINB 1
 #endif
 template <typename T, int KK, int FK, bool VEC>
-__global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
+__global__ __launch_bounds__(k3g_nt<T>(), PCS_3DG_MINB) void k_pds3d_gen(const T* __restrict__ x, T* __restrict__ xn,
                                                      const T* __restrict__ z, T* __restrict__ zn,
                                                      const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk, int edge,
                                                      double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
                                                      int tiles1, int tiles2, Bands bd, int ntasks) {
-  constexpr int T1 = k3g_rows<T>(), TW = k3gTW, NT = k3gNT;
+  constexpr int T1 = k3g_rows<T>(), TW = k3gTW, NT = k3g_nt<T>();
   constexpr int UR = T1 + 2, UG = TW / 4 + 2, WU = 4 * UG;  // u / z0 region: rows r1-1 .. r1+T1, cols c2-4 ..
   constexpr int R1 = T1 + 4, W2G = UG + 2, W2 = 4 * W2G;    // z1 rows r1-2 .. r1+T1+1; z2 cols c2-8 .. c2+TW+8
   constexpr int NU = UR * UG, NZ1 = R1 * UG, NZ2 = UR * W2G, NZ = T1 * (TW / 4);
@@ -637,12 +650,16 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
   const int i1z = r1 + zi, c_z = c2 + 4 * zg;
   // the tile's u region (rows r1-1 .. r1+T1, cols c2-4 .. c2+TW+3) >= 2 samples inside the plane
   // the tile's u region (rows r1-1 .. r1+T1, cols c2-4 .. c2+TW+3) >= 2 samples inside the plane
-  const bool tile_int = r1 - 1 >= 2 && r1 + T1 <= v.n1 - 3 && c2 - 4 >= 2 && c2 + TW + 3 <= v.n2 - 3;
+  const bool row_int = r1 - 1 >= 2 && r1 + T1 <= v.n1 - 3, col_int = c2 - 4 >= 2 && c2 + TW + 3 <= v.n2 - 3;
+  const bool tile_int = row_int && col_int;
+  // a tile on a column border only (most border tiles: every plane row has two) keeps the row axis interior
+  const bool row_only = PCS_3DG_ROWFORM && row_int && !col_int;
 
   // loads run two planes ahead: iteration p lands set p & 1 and refills it with plane p + 2's data
   // (C4 centred: 1.41 ms with one set; the wait for the next plane's loads was exposed at two waves
   // per SIMD)
-  G4<T> xr[2][KU], gr[2][KU], z0r[2][KU], z1r[2][K1], z2r[2][K2];
+  constexpr int NSET = k3g_sets<T>();  // register sets of prefetched planes (loads run NSET planes ahead)
+  G4<T> xr[NSET][KU], gr[NSET][KU], z0r[NSET][KU], z1r[NSET][K1], z2r[NSET][K2];
   auto prefetch = [&](int p, auto sc) {  // x, g, z1, z2 of plane p; z0 of plane p + 1 -> set sc
     constexpr int S = decltype(sc)::value;
     const Rsrc rx = plane_rsrc(x, v, v.hx, p), rz0 = plane_rsrc(z, v, v.hz, p + 1),
@@ -689,7 +706,8 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
     }
   }
   prefetch(p_start - 1, S0{});
-  if (p_start <= p_end) prefetch(p_start, S1{});
+  if constexpr (NSET == 2)
+    if (p_start <= p_end) prefetch(p_start, S1{});
   auto iter = [&](int p, auto sc) {
     constexpr int S = decltype(sc)::value;
     const int sm1 = slot3(p - 1), s0 = slot3(p), sp1 = slot3(p + 1), sm2 = slot3(p - 2);
@@ -703,7 +721,7 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
         if constexpr (FK != PCS_F_NULL) gv4[k] = gr[S][k];
       }
       land(sp1, b2, sc);
-      if (p + 2 <= p_end) prefetch(p + 2, sc);
+      if (p + NSET <= p_end) prefetch(p + NSET, sc);
       lds_barrier();
       // ---- U items: x_t, u on the u region of plane p; x' on own voxels (I: every sample of the
       // tile's u region and plane p lies >= 2 samples inside the volume -- no edge rules)
@@ -764,6 +782,7 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
       using Ff = std::false_type;
       const bool pint_u = gp >= 2 && gp <= v.n0 - 3;
       if (tile_int && pint_u) u_items(Tt{}, Tt{}, Tt{});
+      else if (row_only && pint_u) u_items(Tt{}, Tt{}, Ff{});
       else if (pint_u) u_items(Tt{}, Ff{}, Ff{});
       else u_items(Ff{}, Ff{}, Ff{});
       lds_barrier();
@@ -827,12 +846,17 @@ __global__ __launch_bounds__(k3gNT, PCS_3DG_MINB) void k_pds3d_gen(const T* __re
       };
       const bool pint_z = gp - 1 >= 2 && gp - 1 <= v.n0 - 3;
       if (tile_int && pint_z) z_items(Tt{}, Tt{}, Tt{});
+      else if (row_only && pint_z) z_items(Tt{}, Tt{}, Ff{});
       else if (pint_z) z_items(Tt{}, Ff{}, Ff{});
       else z_items(Ff{}, Ff{}, Ff{});
   };
-  for (int p = p_start - 1; p <= p_end; p += 2) {
-    iter(p, S0{});
-    if (p + 1 <= p_end) iter(p + 1, S1{});
+  if constexpr (NSET == 2) {
+    for (int p = p_start - 1; p <= p_end; p += 2) {
+      iter(p, S0{});
+      if (p + 1 <= p_end) iter(p + 1, S1{});
+    }
+  } else {
+    for (int p = p_start - 1; p <= p_end; ++p) iter(p, S0{});
   }
   block_sum<4>(part, red);
   if (hist != nullptr) {
@@ -947,7 +971,7 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
     if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
       auto kern =
           a->kkind == PCS_BACKWARD ? k_pds3d_gen<T, PCS_BACKWARD, FK, VEC> : k_pds3d_gen<T, PCS_CENTERED, FK, VEC>;
-      kern<<<(unsigned)p.ntasks, k3gNT, 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g,
+      kern<<<(unsigned)p.ntasks, k3g_nt<T>(), 0, st>>>((const T*)a->x, (T*)a->xn, (const T*)a->z, (T*)a->zn, (const T*)a->g,
                                                  v, P, a->hkind, a->gkind, a->edge, a->partials, (Ctrl*)a->ctrl,
                                                  a->hist, a->ws, p.tiles1, p.tiles2, p.bd, p.ntasks);
       return launch_status();
