@@ -561,22 +561,30 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
 // same arithmetic for every voxel (no interior specialisation), so slabs are bitwise the whole
 // volume.  Traffic per voxel: x, g, z (3) in; x', z' (3) out = 9 words (the forward kernel's),
 // plus the tile halos (rows +- 1, one 4-group per side).
-// Tile rows: 16 for fp32 (vertical halo 2/16: PMC reads 1.39x -> ~1.24x the algorithmic at 8 rows;
-// 101 KB of LDS), 12 for fp64 (155.5 KB; 16 rows would need 202 KB.  C5 centred: 17.1 ms against 18.4 at
-// 8 rows, reads 1.45x -> ~1.33x the algorithmic; 10 rows measured 20.0 ms, profiles/r6_g64rows_ab.txt)
+// Tiles: fp64 12 x 128 (155.5 KB of LDS; 16 rows would need 202 KB.  C5 centred: 17.1 ms against 18.4 at
+// 8 rows, reads 1.45x -> ~1.33x the algorithmic; 10 rows measured 20.0 ms, profiles/r6_g64rows_ab.txt).
+// fp32 12 x 256 in 1024-thread workgroups with one prefetch register set (150 KB, 109-128 VGPRs): every
+// row segment a tile reads is 1 KB, as the fp64 tiles' are -- C4 centred 1.075 ms against 1.267 for 16 x 128
+// (512 threads, two sets; 512-B segments, about the same halo share) and 1.22 for 8 x 256
+// (profiles/r6_g32w_ab.txt); 16 x 128 at 1024 threads alone changed nothing (r6_g32nt_ab.txt), so the row
+// segment length, not latency hiding, was what held the fp32 kernel at ~4.4 TB/s
 #ifndef PCS_3DG_NT32  // fp32 workgroup size (diagnostics builds override)
-#define PCS_3DG_NT32 512
+#define PCS_3DG_NT32 1024
 #endif
-constexpr int k3gTW = 128;
+#ifndef PCS_3DG_TW32  // fp32 tile columns (diagnostics builds override)
+#define PCS_3DG_TW32 256
+#endif
+template <typename T>
+constexpr int k3g_tw() { return sizeof(T) == 4 ? PCS_3DG_TW32 : 128; }
 template <typename T>
 constexpr int k3g_nt() { return sizeof(T) == 4 ? PCS_3DG_NT32 : 512; }
 #ifndef PCS_3DG_SETS32  // fp32 prefetch register sets (diagnostics builds override)
-#define PCS_3DG_SETS32 2
+#define PCS_3DG_SETS32 1
 #endif
 template <typename T>
 constexpr int k3g_sets() { return sizeof(T) == 4 ? PCS_3DG_SETS32 : 2; }
 #ifndef PCS_3DG_ROWS32  // fp32 tile rows (diagnostics builds override)
-#define PCS_3DG_ROWS32 16
+#define PCS_3DG_ROWS32 12
 #endif
 #ifndef PCS_3DG_ROWS64  // fp64 tile rows (diagnostics builds override)
 #define PCS_3DG_ROWS64 12
@@ -596,7 +604,7 @@ __global__ __launch_bounds__(k3g_nt<T>(), PCS_3DG_MINB) void k_pds3d_gen(const T
                                                      const T* __restrict__ g, Vol v, P3<T> P, int hk, int gk, int edge,
                                                      double* __restrict__ partials, Ctrl* ctrl, double* hist, void* ws,
                                                      int tiles1, int tiles2, Bands bd, int ntasks) {
-  constexpr int T1 = k3g_rows<T>(), TW = k3gTW, NT = k3g_nt<T>();
+  constexpr int T1 = k3g_rows<T>(), TW = k3g_tw<T>(), NT = k3g_nt<T>();
   constexpr int UR = T1 + 2, UG = TW / 4 + 2, WU = 4 * UG;  // u / z0 region: rows r1-1 .. r1+T1, cols c2-4 ..
   constexpr int R1 = T1 + 4, W2G = UG + 2, W2 = 4 * W2G;    // z1 rows r1-2 .. r1+T1+1; z2 cols c2-8 .. c2+TW+8
   constexpr int NU = UR * UG, NZ1 = R1 * UG, NZ2 = UR * W2G, NZ = T1 * (TW / 4);
@@ -889,9 +897,8 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
   if (pb.b0 == pb.a0) pb = PlaneBands{pb.a1, pb.b1, pb.b1, pb.b1};
   const int t1 = tile_rows3(a);
   p.tiles1 = (int)((a->n1 + t1 - 1) / t1);
-  const int tw = (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) ? k3gTW
-                 : a->dtype == PCS_F32                                  ? K3<float>::TW
-                                                                        : K3<double>::TW;
+  const bool gen = a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED, f32 = a->dtype == PCS_F32;
+  const int tw = gen ? (f32 ? k3g_tw<float>() : k3g_tw<double>()) : f32 ? K3<float>::TW : K3<double>::TW;
   p.tiles2 = (int)((a->n2 + tw - 1) / tw);
   const int64_t per_plane = (int64_t)p.tiles1 * p.tiles2;
   const int64_t L0 = pb.b0 - pb.a0, L1 = pb.b1 - pb.a1, L = L0 + L1;
@@ -966,7 +973,6 @@ static int launch3(const pcs_pds3d_args* a, PlaneBands pb, hipStream_t st) {
   }
   P.seg_a = (T)a->seg_a;
   P.seg_b = (T)a->seg_b;
-  static_assert(k3gTW == k3TW, "the general-K kernel keeps the fp32 forward kernel's column tiles");
   if constexpr (FK != PCS_F_CONV0) {
     if (a->kkind == PCS_BACKWARD || a->kkind == PCS_CENTERED) {
       auto kern =
