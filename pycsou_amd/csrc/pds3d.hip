@@ -932,6 +932,11 @@ static Plan3 plan3(const pcs_pds3d_args* a, PlaneBands pb) {
     const int64_t cost = (tasks + target - 1) / target * (sl + 2);
     if (best < 0 || cost < best) best = cost, nseg = ns;
   }
+  static const int64_t force_seg = [] {
+    const char* e = getenv("PCS_3D_NSEG");  // diagnostics: segment-count sweep
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  if (force_seg > 0) nseg = force_seg < bands ? bands : force_seg > max_seg ? max_seg : force_seg;
   const int64_t seg_len = (L + nseg - 1) / nseg;
   const int64_t n0 = seg_len ? (L0 + seg_len - 1) / seg_len : 0, n1 = seg_len ? (L1 + seg_len - 1) / seg_len : 0;
   p.bd = Bands{(int)seg_len, (int)n0, (int)pb.a0, (int)pb.b0, (int)pb.a1, (int)pb.b1};
