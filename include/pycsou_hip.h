@@ -178,6 +178,13 @@ int pcs_fenchel_l21_pixel(int dtype, const void* w, void* out, int64_t npix, int
  * [0, ngroups) (np.unique order); ws = ngroups doubles. */
 int pcs_prox_l21_labels(int dtype, const void* x, void* out, int64_t n, const int32_t* gid, int64_t ngroups,
                         double tau, void* ws, hipStream_t stream);
+/* The same prox with run-to-run identical group sums (ABI 10; replaces pcs_prox_l21_labels in
+ * L21Norm.prox, func/penalty.py:525-560): `order[n]` lists the elements group by group (a stable
+ * argsort of gid), `off[ngroups + 1]` the group boundaries in it, `maxlen` the largest group; each
+ * group's sum of squares is taken in ascending element order (fp64) without atomics. */
+int pcs_prox_l21_groups(int dtype, const void* x, void* out, int64_t n, const int32_t* gid, int64_t ngroups,
+                        const int32_t* order, const int64_t* off, int64_t maxlen, double tau, void* ws,
+                        hipStream_t stream);
 /* L2Norm.prox (func/penalty.py:23-70 via LpNorm.prox + proj_l2_ball, math/prox.py:207-210):
  * v = x/tau; out = x - tau*(||v|| <= 1 ? v : v/||v||), with ||x||^2 read from the device
  * double `sumsq_dev` (pcs_reduce kind 0). */

@@ -125,6 +125,7 @@ _SIGS = {
     'pcs_prox_l21_pixel': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_int, _c_dbl, _vp]),
     'pcs_fenchel_l21_pixel': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_int, _c_dbl, _c_dbl, _vp]),
     'pcs_prox_l21_labels': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp, _c_i64, _c_dbl, _vp, _vp]),
+    'pcs_prox_l21_groups': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _c_dbl, _vp, _vp]),
     'pcs_prox_l2': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp, _vp]),
     'pcs_prox_sql2': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_dbl, _vp]),
     'pcs_proj_nonneg': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
@@ -196,7 +197,7 @@ class HipError(ValueError):
 
 
 # the argument-struct layout these declarations assume (pcs_abi_version(), include/pycsou_hip.h)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 def load():

@@ -198,6 +198,17 @@ def prox_l21_labels(x, tau, gid, ngroups):
     return out
 
 
+def prox_l21_groups(x, tau, gid, ngroups, order, off, maxlen):
+    """L21Norm.prox over general labels with deterministic group sums (pcs_prox_l21_groups)."""
+    lib = L.gpu()
+    out = torch.empty_like(x)
+    ws = torch.empty(int(ngroups), dtype=torch.float64, device=x.device)
+    L.check(lib.pcs_prox_l21_groups(L.dtcode(x), L.ptr(x), L.ptr(out), x.numel(), L.ptr(gid), int(ngroups),
+                                    L.ptr(order), L.ptr(off), int(maxlen), float(tau), L.ptr(ws), L.stream()),
+            'pcs_prox_l21_groups')
+    return out
+
+
 def prox_l2(x, tau):
     lib = L.gpu()
     ss = reduce_dev(0, x)

@@ -159,7 +159,7 @@ __device__ __forceinline__ void tl_st(double* a, int r, int g, const G4<double>&
 #endif
 // 8 x 128 tiles: a 64-column tile's one-group right halo costs a third 128-B line per row
 // (PMC: 1.53x the algorithmic reads); at 128 columns it is one line in five
-constexpr int k3T1 = 8, k3TW = PCS_K3TW;
+constexpr int k3T1 = 8;
 // fp64 forward-K tile rows (diagnostics builds override): 12 (113.5 KB of LDS, one 512-thread workgroup per
 // CU as at 8) -- C5 update 13.83 against 14.22 ms at 8 (profiles/r6_f3rows_ab.txt)
 #ifndef PCS_3D_ROWS64

@@ -79,6 +79,41 @@ __global__ void k_group_sumsq(const T* __restrict__ x, const int32_t* __restrict
   }
 }
 
+// deterministic group sums (ABI 10): the members of group g are x[order[off[g] .. off[g+1])] in ascending
+// element order (a stable argsort of the labels, formed once by the host), summed in that order in fp64 by
+// one thread per group (short groups) or by one wave per group (lane-strided partial sums, then a fixed
+// butterfly) -- the same sums on every run, unlike the atomic form above
+template <typename T>
+__global__ void k_group_sumsq_thread(const T* __restrict__ x, const int32_t* __restrict__ order,
+                                     const int64_t* __restrict__ off, int64_t ngroups, double* __restrict__ acc) {
+  PCS_GRID_LOOP(g, ngroups) {
+    double s = 0.0;
+    for (int64_t k = off[g]; k < off[g + 1]; ++k) {
+      const double v = (double)x[order[k]];
+      s += v * v;
+    }
+    acc[g] = s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_group_sumsq_wave(const T* __restrict__ x, const int32_t* __restrict__ order,
+                                                          const int64_t* __restrict__ off, int64_t ngroups,
+                                                          double* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ngroups; g += nw) {
+    double s = 0.0;
+    for (int64_t k = off[g] + lane; k < off[g + 1]; k += 64) {
+      const double v = (double)x[order[k]];
+      s += v * v;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane == 0) acc[g] = s;
+  }
+}
+
 template <typename T>
 __global__ void k_group_scale(const T* __restrict__ x, const int32_t* __restrict__ gid, int64_t n,
                               const double* __restrict__ acc, T tau, T* __restrict__ out) {
@@ -318,6 +353,22 @@ int pcs_prox_l21_labels(int dt, const void* x, void* out, int64_t n, const int32
   PCS_DISPATCH(dt, k_group_sumsq<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, gid, n, (double*)ws);
                k_group_scale<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, gid, n, (const double*)ws, (T)tau,
                                                                   (T*)out));
+  return launch_status();
+}
+
+int pcs_prox_l21_groups(int dt, const void* x, void* out, int64_t n, const int32_t* gid, int64_t ngroups,
+                        const int32_t* order, const int64_t* off, int64_t maxlen, double tau, void* ws, hipStream_t st) {
+  if (!x || !out || !gid || !order || !off || !ws || n < 0 || ngroups < 1 || maxlen < 0) return PCS_EINVAL;
+  if (maxlen <= 32) {
+    PCS_DISPATCH(dt, k_group_sumsq_thread<T><<<grid_for(ngroups, 256), 256, 0, st>>>((const T*)x, order, off, ngroups,
+                                                                                    (double*)ws));
+  } else {
+    const int64_t nb = (ngroups + 3) / 4;
+    PCS_DISPATCH(dt, k_group_sumsq_wave<T><<<(unsigned)(nb < 65536 ? nb : 65536), 256, 0, st>>>(
+                         (const T*)x, order, off, ngroups, (double*)ws));
+  }
+  PCS_DISPATCH(dt, k_group_scale<T><<<grid_for(n, 256), 256, 0, st>>>((const T*)x, gid, n, (const double*)ws, (T)tau,
+                                                                      (T*)out));
   return launch_status();
 }
 

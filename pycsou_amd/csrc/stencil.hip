@@ -206,7 +206,7 @@ using namespace pcs;
 
 extern "C" {
 
-int pcs_abi_version(void) { return 9; }  // 9: pcs_slab2d_deep_* (communication-avoiding slab loop), pcs_pds_reduce_finalize_k; 8: pcs_pds2d_args fin_partials, pcs_pds_finalize_pending; 7: the persistent 2-D loop (pcs_pds2d_run_persistent, pcs_grid_bar_bytes) removed; 6: pcs_pds2d_args mkind, ym, zm, zmn; 2: pcs_pds2d_args gained kkind, edge, w0, w1; 3: conv_fwd, conv_adj, conv_tier, rbuf; 4: pcs_pds3d_args kkind, edge; 5: pcs_pds3d_args conv0_*
+int pcs_abi_version(void) { return 10; }  // 10: pcs_prox_l21_groups (deterministic label sums); 9: pcs_slab2d_deep_* (communication-avoiding slab loop), pcs_pds_reduce_finalize_k; 8: pcs_pds2d_args fin_partials, pcs_pds_finalize_pending; 7: the persistent 2-D loop (pcs_pds2d_run_persistent, pcs_grid_bar_bytes) removed; 6: pcs_pds2d_args mkind, ym, zm, zmn; 2: pcs_pds2d_args gained kkind, edge, w0, w1; 3: conv_fwd, conv_adj, conv_tier, rbuf; 4: pcs_pds3d_args kkind, edge; 5: pcs_pds3d_args conv0_*
 
 int pcs_deriv1_fwd(int dt, const void* x, void* out, int ndim, const int64_t* dims, int axis, double step, int kind,
                    int edge, hipStream_t st) {

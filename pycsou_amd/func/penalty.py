@@ -137,6 +137,7 @@ class L21Norm(LpNorm):
             self.pixel_d = _is_pixel_grouping(self.groups, dim)   # d > 0 -> per-pixel kernel
             self._inv = inv.astype(np.int32)
         self._gid = None
+        self._csr = None
 
     def _gid_dev(self):
         if self._gid is None:
@@ -153,10 +154,25 @@ class L21Norm(LpNorm):
         ss.index_add_(0, self._gid_dev().long(), t.double() ** 2)
         return float(torch.sqrt(ss).sum())
 
+    def _csr_dev(self):
+        """(order, offsets, largest group) of the labels on the device: the elements group by group in
+        ascending element order, for the deterministic group sums of pcs_prox_l21_groups."""
+        if getattr(self, '_csr', None) is None:
+            gid = self._gid_dev()
+            inv = self._inv
+            order = np.argsort(inv, kind='stable').astype(np.int32)
+            counts = np.bincount(inv, minlength=self.groups_idxs.size)
+            off = np.zeros(counts.size + 1, dtype=np.int64)
+            np.cumsum(counts, out=off[1:])
+            self._csr = (torch.as_tensor(order).to(gid.device), torch.as_tensor(off).to(gid.device),
+                         int(counts.max()) if counts.size else 0)
+        return self._csr
+
     def _prox(self, t, tau):
         if self.pixel_d:
             return O.prox_l21_pixel(t, tau, self.pixel_d)
-        return O.prox_l21_labels(t, tau, self._gid_dev(), self.groups_idxs.size)
+        order, off, maxlen = self._csr_dev()
+        return O.prox_l21_groups(t, tau, self._gid_dev(), self.groups_idxs.size, order, off, maxlen)
 
     def _fenchel_scaled(self, w, sigma, lam):
         if self.pixel_d:

@@ -14,6 +14,7 @@ reference iteration operator by operator on the GPU kernels (``update_iterand`` 
 with the diagnostics norms reduced on the device.
 """
 
+import os
 from numbers import Number
 
 import numpy as np
@@ -82,12 +83,12 @@ class _DeviceLoop:
     # max_iter of 1e9 with accuracy_threshold doing the stopping must not allocate 16 GB up front)
     HIST_CHUNK = 4096
 
-    def __init__(self, max_iter, min_iter, thr, has_dual, device, lag=3):
+    def __init__(self, max_iter, min_iter, thr, has_dual, device, lag=3, cap=None):
         from .. import _lib as L
         self.L, self.lib = L, L.gpu()
         max_iter, min_iter = int(max_iter), int(min_iter)
         self.total = max(min_iter, max_iter) + 1
-        cap = min(self.total, self.HIST_CHUNK)
+        cap = min(self.total, self.HIST_CHUNK) if cap is None else int(cap)  # cap: rows up front (graph chunks)
         self.hist = torch.full((2 * cap + 2,), float('nan'), dtype=torch.float64, device=device)
         self.ctrl = torch.zeros(int(self.lib.pcs_ctrl_bytes()) // 8, dtype=torch.float64, device=device)
         self.sums = torch.zeros(4, dtype=torch.float64, device=device)
@@ -130,6 +131,16 @@ class _DeviceLoop:
         ev = torch.cuda.Event()
         ev.record()
         self.pending.append((host, ev))
+
+    def record_captured(self, x_old, x, z_old=None, z=None):
+        """``record`` inside a graph capture: the sums and the loop control only (no read-back, no
+        growth -- the history holds every row up front, ``cap``)."""
+        L = self.L
+        O.rel_sums(x_old, x, self.sums[0:2])
+        if self.has_dual:
+            O.rel_sums(z_old, z, self.sums[2:4])
+        L.check(self.lib.pcs_pds_finalize(L.ptr(self.sums), L.ptr(self.ctrl), L.ptr(self.hist), L.stream()),
+                'pcs_pds_finalize')
 
     def stream_rows(self, every, show):
         """``verbose``: show(k, row) for every resolved iteration k with k % every == 0, while the
@@ -340,6 +351,11 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
         state = {'primal_variable': O.to_dev(self.x0, dtype),
                  'dual_variable': None if self.z0 is None else O.to_dev(self.z0, dtype)}
         self.init_iterand_dev = dict(state)
+        self._graph_used = False
+        if self._graph_ok(state):
+            out = self._iterate_generic_graph(state)
+            if out is not None:
+                return out
         loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, bool(self._H),
                            state['primal_variable'].device)
         if self.verbose is not None:
@@ -373,8 +389,112 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
                         'dual_variable': self._out(self._state['dual_variable'])}
         return self.iterand, self.converged, self.diagnostics
 
-    def _update_dev(self, st):
-        """``PrimalDualSplitting.update_iterand`` (proxalgs.py:343-355) on device tensors."""
+    # iterations per captured chunk of the generic path; the state ring holds two chunks
+    GRAPH_CHUNK = 4
+    GRAPH_RING_BYTES = 8 << 30
+
+    def _graph_ok(self, state):
+        """The generic loop runs as hipGraph chunks (``_iterate_generic_graph``) on a GPU unless
+        PCS_GENERIC_GRAPH=0, when the state ring fits GRAPH_RING_BYTES and the history fits up front."""
+        x = state['primal_variable']
+        if os.environ.get('PCS_GENERIC_GRAPH', '1') == '0' or x.device.type != 'cuda':
+            return False
+        nbytes = sum(t.numel() * t.element_size() for t in state.values() if t is not None)
+        total = max(int(self.max_iter), int(self.min_iter)) + 1
+        return 2 * self.GRAPH_CHUNK * nbytes <= self.GRAPH_RING_BYTES and total <= (1 << 22)
+
+    def _iterate_generic_graph(self, state):
+        """The generic loop with its per-iteration launches captured: two hipGraphs of GRAPH_CHUNK
+        iterations each write a ring of 2 x GRAPH_CHUNK states (iteration i -> slot i mod 2C, reading
+        slot i - 1) and end with an asynchronous read-back of the loop control; they alternate, at
+        most one chunk runs ahead of the one whose read-back the host waits for, so the state of the
+        stopping iteration (always in the chunk that reports the stop) is never overwritten.
+        Iterations past the stop are computed and discarded, as in the eager path (the finalize
+        kernel ignores them).  The same launches as the eager loop, so the iterates and the
+        diagnostics are bitwise the eager path's.  None if the capture fails (the eager path runs)."""
+        C = self.GRAPH_CHUNK
+        R = 2 * C
+        x0, z0 = state['primal_variable'], state['dual_variable']
+        total = max(int(self.max_iter), int(self.min_iter)) + 1
+        loop = _DeviceLoop(self.max_iter, self.min_iter, self.accuracy_threshold, bool(self._H), x0.device,
+                           cap=total + R + 2)
+        X = [torch.empty_like(x0) for _ in range(R)]
+        Z = [None if z0 is None else torch.empty_like(z0) for _ in range(R)]
+        X[R - 1].copy_(x0)
+        if z0 is not None:
+            Z[R - 1].copy_(z0)
+        # one eager iteration and reduction first (discarded): lazy library state (plans, workspaces) is
+        # created outside the capture
+        self._update_dev({'primal_variable': X[R - 1], 'dual_variable': Z[R - 1]})
+        O.rel_sums(X[R - 1], X[R - 1], loop.sums[0:2])
+        host = [torch.zeros(2, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        graphs, pool = [], None
+        try:
+            for h in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    for j in range(C):
+                        slot, prev = h * C + j, (h * C + j - 1) % R
+                        self._update_dev({'primal_variable': X[prev], 'dual_variable': Z[prev]},
+                                         out=(X[slot], Z[slot] if self._H else None))
+                        loop.record_captured(X[prev], X[slot], Z[prev], Z[slot])
+                    host[h].copy_(loop.ctrl.view(torch.int32)[:2], non_blocking=True)
+                pool = g.pool()
+                graphs.append(g)
+        except Exception:  # noqa: BLE001 -- torch's capture errors and the ABI's HipError alike
+            torch.cuda.synchronize()
+            return None
+        self._graph_used = True
+        show = None
+        if self.verbose is not None:
+            every = int(self.verbose)
+
+            def show(lo, hi):
+                for k in range(lo, hi):
+                    if k % every == 0:
+                        h = loop.hist[2 * k:2 * k + 2].cpu().numpy()
+                        self._rows = [[k, h[0], h[1]] if self._H else [k, h[0]]]
+                        self.print_diagnostics()
+        max_chunks = -(-total // C) + 2  # the control stops the loop by then (max_iter, history length)
+        inflight, k, n, shown = [], 0, None, 0
+        while n is None:
+            if k < max_chunks:
+                graphs[k % 2].replay()
+                ev = torch.cuda.Event()
+                ev.record()
+                inflight.append((k, ev))
+                k += 1
+            if len(inflight) >= 2 or (k >= max_chunks and inflight):
+                kc, ev = inflight.pop(0)
+                ev.synchronize()
+                it, stopped = int(host[kc % 2][0]), int(host[kc % 2][1])
+                if show is not None:
+                    show(shown, it)
+                    shown = it
+                if stopped:
+                    n = it
+            elif k >= max_chunks:
+                raise RuntimeError('generic PDS loop: the device control never stopped')
+        torch.cuda.synchronize()  # the chunk run ahead of the stop has finished with the ring
+        self.iter = n
+        h = loop.rows(n)
+        self._rows = [[i, h[i, 0], h[i, 1]] if self._H else [i, h[i, 0]] for i in range(n)]
+        last = (n - 1) % R
+        self._state = {'primal_variable': X[last], 'dual_variable': Z[last] if self._H else None}
+        self.converged = True
+        cols = ['Iter', 'Relative Improvement (primal variable)']
+        if self._H:
+            cols.append('Relative Improvement (dual variable)')
+        self.diagnostics = _frame(cols, self._rows)
+        self.iterand = {'primal_variable': self._out(self._state['primal_variable']),
+                        'dual_variable': self._out(self._state['dual_variable'])}
+        return self.iterand, self.converged, self.diagnostics
+
+    def _update_dev(self, st, out=None):
+        """``PrimalDualSplitting.update_iterand`` (proxalgs.py:343-355) on device tensors (``out``: the
+        (x, z) buffers the relaxation steps write)."""
+        ox, oz = (None, None) if out is None else out
         x, z = st['primal_variable'], st['dual_variable']
         g = self.F._grad(x)
         if self._H:
@@ -386,8 +506,8 @@ class PrimalDualSplitting(GenericIterativeAlgorithm):
             u = O.axpby(x_temp, x, 2.0, -1.0)
             w = O.axpby(z, self.K._apply(u), 1.0, self.sigma)
             z_temp = self.H._fenchel(w, self.sigma)
-            z = O.axpby(z_temp, z, self.rho, 1 - self.rho)
-        x = O.axpby(x_temp, x, self.rho, 1 - self.rho)
+            z = O.axpby(z_temp, z, self.rho, 1 - self.rho, out=oz)
+        x = O.axpby(x_temp, x, self.rho, 1 - self.rho, out=ox)
         return {'primal_variable': x, 'dual_variable': z}
 
     def update_iterand(self):

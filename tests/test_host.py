@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert declared <= set(_lib.EXPORTS), declared - set(_lib.EXPORTS)
-    assert lib.pcs_abi_version() == 9
+    assert lib.pcs_abi_version() == 10
     assert lib.pcs_ctrl_bytes() == 64
     assert lib.pcs_pds2d_halo_x(7) == 15
 

@@ -65,7 +65,8 @@ def launches(mk, it):
 
 def main():
     torch.cuda.set_device(0)
-    n, W, K = 2048, 20, 200
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048  # image side (256: the launch-bound regime)
+    W, K = 20, 200
     for dtype in (torch.float32, torch.float64):
         for name in ('l21_labels', 'stack_h'):
             t0 = time.perf_counter()
