@@ -459,7 +459,8 @@ def test_pds3d_folded_axis0_bitwise(monkeypatch, shape):
 
 @pytest.mark.parametrize('shape,dtype,kind', [((20, 36, 260), np.float64, 'centered'), ((17, 9, 132), np.float32, 'centered'),
                                               ((12, 33, 130), np.float64, 'backward'), ((24, 20, 24), np.float32, 'backward'),
-                                              ((12, 40, 136), np.float32, 'centered')])
+                                              ((12, 40, 136), np.float32, 'centered'), ((10, 30, 260), np.float32, 'centered'),
+                                              ((9, 26, 258), np.float32, 'backward'), ((8, 30, 66), np.float64, 'centered')])
 def test_pds3d_general_k_vs_oracle(shape, dtype, kind):
     """Backward / centred 3-D Gradient (the reference's default kind) through the general-K plane
     march (k_pds3d_gen): ragged tiles (last column tile of 4 or 2 columns, rows not a multiple of
