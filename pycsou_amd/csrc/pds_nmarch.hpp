@@ -158,6 +158,11 @@ __device__ __forceinline__ float oct_sum8(float v) {
 #ifndef PCS_NMG_ABL
 #define PCS_NMG_ABL 0
 #endif
+// GEN: the border strips' steps with interior rows take a form with the row axis interior (only the column
+// axis on the edge rules) -- 0: every non-interior step on the all-axes form (A/B knob)
+#ifndef PCS_NMG_ROWFORM
+#define PCS_NMG_ROWFORM 1
+#endif
 // GEN: backward / centred K (KK != PCS_FORWARD) -- K^T z reads z rows lr - 1 .. lr + 1 and columns
 // c - 1 .. c + 1, K u reads u rows r - 1 .. r + 1 and columns c - 1 .. c + 1: z tiles of 18 rows (the
 // z0 tile from column c0 - 4 too), an 18-row u ring, and a sixth u / t / g column c0 - 1 (group 0,
@@ -537,21 +542,23 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
       const bool own = lr >= s0 && lr < s1 && gr < n0 && cown;
       // x_t = prox_G((x - tau (g - b)) - tau K^T z), K^T z = D0^T z0 + D1^T z1 (stencil.hpp windows;
       // I: rows and columns >= 2 samples inside the image, no edge rules -- the same bits)
-      auto xt_of = [&](auto intc, T gd, T xv, const T (&w0)[5], const T (&w1)[5], int i1) {
-        constexpr bool I = decltype(intc)::value || (PCS_NMG_ABL & 2);
-        const T kt = pcs_fma(sw_d1_adj<KK, I>(w0, gr, n0, edge), P.inv_step0,
-                             sw_d1_adj<KK, I>(w1, i1, n1, edge) * P.inv_step1);
+      // (intr: the row axis interior; intc: the column axis)
+      auto xt_of = [&](auto intr, auto intc, T gd, T xv, const T (&w0)[5], const T (&w1)[5], int i1) {
+        constexpr bool I0 = decltype(intr)::value || (PCS_NMG_ABL & 2);
+        constexpr bool I1 = decltype(intc)::value || (PCS_NMG_ABL & 2);
+        const T kt = pcs_fma(sw_d1_adj<KK, I0>(w0, gr, n0, edge), P.inv_step0,
+                             sw_d1_adj<KK, I1>(w1, i1, n1, edge) * P.inv_step1);
         return prox_g((xv - P.tau * gd) - P.tau * kt, gk, P.seg_a, P.seg_b);
       };
       G4<T> uo, xo;
       T sdx = T(0), sx = T(0);
-      auto items = [&](auto intc) {
+      auto items = [&](auto intr, auto intc) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const T xv = xv4.v[m];
           const T w0[5] = {T(0), za.v[m], zb.v[m], zc.v[m], T(0)};
           const T w1[5] = {T(0), zh[m], zh[m + 1], zh[m + 2], T(0)};
-          const T xt = xt_of(intc, g.v[m] - bv.v[m], xv, w0, w1, ucg + m);
+          const T xt = xt_of(intr, intc, g.v[m] - bv.v[m], xv, w0, w1, ucg + m);
           uo.v[m] = (rrow && cin) ? (T(2) * xt - xv) : T(0);
           const T xnew = pcs_fma(P.rho, xt, P.omr * xv);
           xo.v[m] = xnew;
@@ -560,8 +567,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
           sx += xv * xv;
         }
       };
-      if (rint && cint) items(std::true_type{});
-      else items(std::false_type{});
+      if (rint && cint) items(std::true_type{}, std::true_type{});
+      else if (PCS_NMG_ROWFORM && rint) items(std::true_type{}, std::false_type{});
+      else items(std::false_type{}, std::false_type{});
       if (own) {
         part[0] += (double)sdx;
         part[1] += (double)sx;
@@ -675,14 +683,15 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
     const bool rint = s.row0 + a >= 2 && s.row0 + a + TS <= n0 - 3;
     G4<T> o0, o1;
     T sdz = T(0), sz = T(0);
-    auto items = [&](auto intc) {
-      constexpr bool I = decltype(intc)::value || (PCS_NMG_ABL & 2);
+    auto items = [&](auto intr, auto intc) {
+      constexpr bool I0 = decltype(intr)::value || (PCS_NMG_ABL & 2);
+      constexpr bool I1 = decltype(intc)::value || (PCS_NMG_ABL & 2);
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const T w0[5] = {T(0), uu.v[m], uc.v[m], ud.v[m], T(0)};
         const T w1[5] = {T(0), uh[m], uh[m + 1], uh[m + 2], T(0)};
-        const T k0 = sw_d1_fwd<KK, I>(w0, gr, n0, P.inv_step0, edge);
-        const T k1 = sw_d1_fwd<KK, I>(w1, ucg + m, n1, P.inv_step1, edge);
+        const T k0 = sw_d1_fwd<KK, I0>(w0, gr, n0, P.inv_step0, edge);
+        const T k1 = sw_d1_fwd<KK, I1>(w1, ucg + m, n1, P.inv_step1, edge);
         const T w0v = zv0.v[m] + P.sigma * k0, w1v = zv1.v[m] + P.sigma * k1;
         T zt0, zt1;
         if (HK == PCS_H_L21) {  // w min(1, lam / ||w||), as p6f
@@ -700,8 +709,9 @@ __device__ __forceinline__ void nmarch_task(const T* __restrict__ x, T* __restri
         sz += pcs_fma(zv0.v[m], zv0.v[m], zv1.v[m] * zv1.v[m]);
       }
     };
-    if (rint && cint) items(std::true_type{});
-    else items(std::false_type{});
+    if (rint && cint) items(std::true_type{}, std::true_type{});
+    else if (PCS_NMG_ROWFORM && rint) items(std::true_type{}, std::false_type{});
+    else items(std::false_type{}, std::false_type{});
     if (own) {
       part[2] += (double)sdz;
       part[3] += (double)sz;
