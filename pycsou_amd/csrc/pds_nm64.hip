@@ -197,8 +197,9 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
   // ---- PV + U: rows lr0 = a + 1 + 2 vi, lr0 + 1, chunk vg; bv: b of those rows; za: the z tiles' first row
   // I (std::true_type): every row and column the phase touches lies >= 2 samples inside the image -- the
   // stencils without their edge rules (stencil.hpp: the same bits)
-  auto pvu = [&](auto intc, int a, const D2 (&bv)[2], int za) {
-    constexpr bool I = decltype(intc)::value;
+  // (intr: the row axis; intc: the column axis)
+  auto pvu = [&](auto intr, auto intc, int a, const D2 (&bv)[2], int za) {
+    constexpr bool I0 = decltype(intr)::value, I1 = decltype(intc)::value;
     const int lr0 = a + 1 + 2 * vi;
     // g = N_v t - b: t rows lr0 - 2H .. lr0 + 1 + 2H, contiguous through the mirror (immediate offsets)
     const T* p0 = TR + M::tslot(lr0 - 2 * H) * TP + 2 * vg;
@@ -275,8 +276,8 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
         const T w0[5] = {T(0), z0w[r].v[m], z0w[r + 1].v[m], z0w[r + 2].v[m], T(0)};  // rows lr - 1 .. lr + 1
         const T z1c[6] = {z1w[r][0].v[0], z1w[r][0].v[1], z1w[r][1].v[0], z1w[r][1].v[1], z1w[r][2].v[0], z1w[r][2].v[1]};
         const T w1[5] = {T(0), z1c[1 + m], z1c[2 + m], z1c[3 + m], T(0)};  // columns c - 1 .. c + 1
-        const T kt = pcs_fma(sw_d1_adj<KK, I>(w0, gr, n0, edge), P.inv_step0,
-                             sw_d1_adj<KK, I>(w1, c, n1, edge) * P.inv_step1);
+        const T kt = pcs_fma(sw_d1_adj<KK, I0>(w0, gr, n0, edge), P.inv_step0,
+                             sw_d1_adj<KK, I1>(w1, c, n1, edge) * P.inv_step1);
         const T xvm = xv2.v[m];
         const T xt = prox_g((xvm - P.tau * gv[r][m]) - P.tau * kt, gk, P.seg_a, P.seg_b);
         uo.v[m] = (rin && c_in) ? (T(2) * xt - xvm) : T(0);
@@ -297,8 +298,8 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
 
   // ---- Z: z' on rows lz0 = a + 2 vi, lz0 + 1, chunk vg; K u from u rows lz0 - 1 .. lz0 + 2 and columns
   // vc - 2 .. vc + 3 of rows lz0, lz0 + 1
-  auto zph = [&](auto intc, int a) {
-    constexpr bool I = decltype(intc)::value;
+  auto zph = [&](auto intr, auto intc, int a) {
+    constexpr bool I0 = decltype(intr)::value, I1 = decltype(intc)::value;
     const int lz0 = a + 2 * vi;
     D2 uw[4], uh[2][3];
 #pragma unroll
@@ -323,8 +324,8 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
         const T w0[5] = {T(0), uw[r].v[m], uw[r + 1].v[m], uw[r + 2].v[m], T(0)};  // rows lr - 1 .. lr + 1
         const T uc[6] = {uh[r][0].v[0], uh[r][0].v[1], uh[r][1].v[0], uh[r][1].v[1], uh[r][2].v[0], uh[r][2].v[1]};
         const T w1[5] = {T(0), uc[1 + m], uc[2 + m], uc[3 + m], T(0)};  // columns c - 1 .. c + 1
-        const T ku0 = sw_d1_fwd<KK, I>(w0, gr, n0, P.inv_step0, edge);
-        const T ku1 = sw_d1_fwd<KK, I>(w1, c, n1, P.inv_step1, edge);
+        const T ku0 = sw_d1_fwd<KK, I0>(w0, gr, n0, P.inv_step0, edge);
+        const T ku1 = sw_d1_fwd<KK, I1>(w1, c, n1, P.inv_step1, edge);
         const T wz0 = zv0.v[m] + P.sigma * ku0, wz1 = zv1.v[m] + P.sigma * ku1;
         const T q0 = wz0 * P.inv_sigma, q1 = wz1 * P.inv_sigma;
         T zt0, zt1;
@@ -383,7 +384,7 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
     }
     if (pr < NPRO) ph(s0 - 1 - 2 * H + pr);
     lds_barrier();
-    if (vi == 15) pvu(std::false_type{}, s0 - TS, bv, s0 - TS);
+    if (vi == 15) pvu(std::false_type{}, std::false_type{}, s0 - TS, bv, s0 - TS);
     __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // step 0's x rows (and row pair 15's x' stores)
     lds_barrier();  // the prologue's U is done with the x ring rows the landing overwrites
     store_x(xnx, s0 + 2 * H + 1, TS);
@@ -395,7 +396,7 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
 #endif
   const bool cint = PCS_NM64_ALLINT || (cb >= 2 && cb + M::CW + 2 <= n1);  // the strip's columns [cb, cb + 64) >= 2 inside
   // one step; RI: its U rows [a + 1, a + 33) and Z rows [a, a + 32) >= 2 inside the image
-  auto step = [&](int a, auto ri) {
+  auto step = [&](int a, auto ri, auto ci) {
     lds_barrier();  // step k - 1 done with the z tiles and the u ring; this step's x rows have landed
     __builtin_amdgcn_s_setprio(3);  // the step's loads issue ahead of other waves' VALU
     load_z(a, 0);
@@ -409,30 +410,41 @@ __device__ __forceinline__ void nm64_task(const double* __restrict__ x, double* 
     ph(a + 2 * H + 1 + pr);
     __builtin_amdgcn_s_waitcnt((NXL & 15) | ((NXL >> 4) << 14) | (7 << 4) | (15 << 8));  // z tiles and b landed
     lds_barrier();
-    pvu(ri, a, bv, a);
+    pvu(ri, ci, a, bv, a);
     lds_barrier();
-    zph(ri, a);
+    zph(ri, ci, a);
     // the next step's x rows (in flight behind: 2 x' and 4 z' stores) into the slots of rows [a + 2H - 15,
     // a + 2H + 17), which this step's PH and U were the last to read
     __builtin_amdgcn_s_waitcnt((6 & 15) | (7 << 4) | (15 << 8));
     store_x(xnx, a + TS + 2 * H + 1, TS);
   };
-  auto rint_of = [&](int a) {
-    return PCS_NM64_ALLINT || (cint && s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0);
-  };
+  auto rows_in = [&](int a) { return PCS_NM64_ALLINT || (s.row0 + a >= 2 && s.row0 + a + TS + 3 <= n0); };
 #ifndef PCS_NM64_PEEL  // diagnostics: 0 = one loop choosing the form per step
 #define PCS_NM64_PEEL 1
 #endif
-  if (PCS_NM64_PEEL && rint_of(s0) && rint_of(s0 + (nsteps - 1) * TS)) {
-    // every step of the task interior (uniform): a loop holding the interior form only -- with both
-    // forms in the loop body the interior steps ran slower (profiles/r5_nm64_split_ab.txt)
-    for (int k = 0; k < nsteps; ++k) step(s0 + k * TS, std::true_type{});
-  } else {
-    for (int k = 0; k < nsteps; ++k) {
-      const int a = s0 + k * TS;
-      if (rint_of(a)) step(a, std::true_type{});
-      else step(a, std::false_type{});
+// the border strips' interior-row steps on a form with the row axis interior (0: the all-axes edge form)
+#ifndef PCS_NM64_ROWFORM
+#define PCS_NM64_ROWFORM 1
+#endif
+  using Tt = std::true_type;
+  using Ff = std::false_type;
+  const bool peel = PCS_NM64_PEEL && rows_in(s0) && rows_in(s0 + (nsteps - 1) * TS);
+  if (cint) {
+    if (peel) {
+      // every step of the task interior (uniform): a loop holding the interior form only -- with both
+      // forms in the loop body the interior steps ran slower (profiles/r5_nm64_split_ab.txt)
+      for (int k = 0; k < nsteps; ++k) step(s0 + k * TS, Tt{}, Tt{});
+    } else {
+      for (int k = 0; k < nsteps; ++k) {
+        const int a = s0 + k * TS;
+        if (rows_in(a)) step(a, Tt{}, Tt{});
+        else step(a, Ff{}, Ff{});
+      }
     }
+  } else if (PCS_NM64_ROWFORM && peel) {  // a border strip whose rows are all interior: the column rules only
+    for (int k = 0; k < nsteps; ++k) step(s0 + k * TS, Tt{}, Ff{});
+  } else {
+    for (int k = 0; k < nsteps; ++k) step(s0 + k * TS, Ff{}, Ff{});
   }
 }
 

@@ -387,6 +387,16 @@ def test_vmcnt_check_sees_every_dma_site():
     # a wait split in two before the barrier: the later, tighter one covers the group
     split = copy_bad[:6] + ['s_waitcnt vmcnt(0)'] + copy_bad[6:]
     assert vc.check_body(split)[0][1]
+    # the control-flow form used by check(): the same verdicts per copy ...
+    cfg = vc.check_body_cfg(copy_bad + ['s_branch .LBB0_1'] + copy_ok)
+    assert [ok for _, ok, _, _ in cfg] == [True, False, True, True]  # per DMA load: the first of a group defers
+    # ... and a DMA loop laid out after the block it exits to (round 6, k_pds2d_nmarch64's tile loop), which
+    # the linear scan misreads: the path from the DMA load runs through the branch to the loads and the wait
+    ool = ['s_cbranch_vccz .LBB0_2', '.LBB0_1:', 'buffer_load_dwordx4 v[4:7], v2, s[4:7], 0 offen',
+           's_waitcnt vmcnt(1)', 's_barrier', 's_endpgm', '.LBB0_2:', 'buffer_load_dwordx4 v0, s[0:3], 0 offen lds',
+           's_cbranch_scc0 .LBB0_1', 's_branch .LBB0_2']
+    assert vc.check_body_cfg(ool)[0][1]
+    assert not vc.check_body_cfg([l.replace('vmcnt(1)', 'vmcnt(2)') for l in ool])[0][1]
 
 
 @pytest.mark.parametrize('spectrum', ['cluster', 'gap'])
