@@ -3,7 +3,7 @@
 # headline roofline is checked against)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r6_bench; mkdir -p $O
+O=gpurun_out/${R6_OUT:-r6_bench}; mkdir -p $O
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
 tail -c 600 $O/bench.json
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_prof.json 2> $O/bench_prof.err || { echo "prof failed"; tail -5 $O/bench_prof.err; exit 1; }
