@@ -418,3 +418,10 @@ def test_lanczos_bound_is_tight_and_safe(spectrum):
     lam = _lanczos_extreme(lambda q: d * q, d.numel(), tol=tol, device='cpu')
     top = float(ev.max())
     assert top * (1 - 1e-12) <= lam <= top * (1 + np.sqrt(tol)), (lam, top)
+
+
+def test_graft_build_entry():
+    """__graft_entry__.build() (the driver's build check, run on CPU) compiles and loads the library whose
+    ABI the bindings expect -- a stale constant there failed it silently for part of round 6."""
+    import __graft_entry__ as g
+    g.build()
