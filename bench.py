@@ -47,7 +47,7 @@ import torch.distributed as dist
 
 METRIC = 'PDS iters/sec on 4096² TV-deconv; achieved HBM GB/s vs roofline at 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-TRAFFIC_JSON = 'profiles/r5_profd_c3_traffic.json'  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the step kernel (tools/prof_r5b.sh)
+TRAFFIC_JSON = 'profiles/r6_profc3_traffic.json'  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the step kernel (tools/prof_nm.sh r6_profc3)
 
 
 def phantom(shape, n_rect, seed):
