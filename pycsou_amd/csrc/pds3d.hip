@@ -576,13 +576,19 @@ __global__ __launch_bounds__(FK == PCS_F_CONV0 ? 2 * K3<T>::NT : K3<T>::NT, FK =
 #endif
 template <typename T>
 constexpr int k3g_tw() { return sizeof(T) == 4 ? PCS_3DG_TW32 : 128; }
+#ifndef PCS_3DG_NT64  // fp64 workgroup size (diagnostics builds override; 1024 with one set spills 98-202 VGPRs)
+#define PCS_3DG_NT64 512
+#endif
 template <typename T>
-constexpr int k3g_nt() { return sizeof(T) == 4 ? PCS_3DG_NT32 : 512; }
+constexpr int k3g_nt() { return sizeof(T) == 4 ? PCS_3DG_NT32 : PCS_3DG_NT64; }
 #ifndef PCS_3DG_SETS32  // fp32 prefetch register sets (diagnostics builds override)
 #define PCS_3DG_SETS32 1
 #endif
+#ifndef PCS_3DG_SETS64  // fp64 prefetch register sets (diagnostics builds override)
+#define PCS_3DG_SETS64 2
+#endif
 template <typename T>
-constexpr int k3g_sets() { return sizeof(T) == 4 ? PCS_3DG_SETS32 : 2; }
+constexpr int k3g_sets() { return sizeof(T) == 4 ? PCS_3DG_SETS32 : PCS_3DG_SETS64; }
 #ifndef PCS_3DG_ROWS32  // fp32 tile rows (diagnostics builds override)
 #define PCS_3DG_ROWS32 12
 #endif
