@@ -275,11 +275,17 @@ static void launch_contig(const T* x, T* out, int64_t rows, int64_t na, const T*
   }
 }
 
-template <typename T, int KT>
+// VP adjacent voxels per thread (one VP-wide load / store per plane and array): the same per-voxel sums
+template <typename T, int VP>
+struct alignas(sizeof(T) * VP) C0Vec {
+  T v[VP];
+};
+template <typename T, int KT, int VP>
 __global__ __launch_bounds__(256) void k_conv0_rta(const T* __restrict__ tin, const T* __restrict__ y, T* __restrict__ s,
                                                    int64_t nsub, int64_t plane, const T* __restrict__ taps, int k,
                                                    int off, int64_t img_lo, int64_t img_hi, int64_t q0, int64_t q1) {
-  const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  using V = C0Vec<T, VP>;
+  const int64_t pos = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VP;  // plane % VP == 0 (host)
   if (pos >= plane) return;
   T h[KT], hf[KT];
 #pragma unroll
@@ -291,36 +297,47 @@ __global__ __launch_bounds__(256) void k_conv0_rta(const T* __restrict__ tin, co
   const int64_t nsteps = (q1 + k - 2) - p0 + 1;
   const int64_t nblk = (nsteps + KT - 1) / KT;
   const int64_t lo = img_lo > 0 ? img_lo : 0, hi = img_hi < nsub ? img_hi : nsub;
-  T tw[KT], rw[KT], tl[KT], yl[KT];
+  T tw[KT][VP], rw[KT][VP];
+  V tl[KT], yl[KT];
 #pragma unroll
-  for (int u = 0; u < KT; ++u) tw[u] = rw[u] = T(0);
-  auto load_blk = [&](int64_t b, T (&tv)[KT], T (&yv)[KT]) {
+  for (int u = 0; u < KT; ++u)
+#pragma unroll
+    for (int m = 0; m < VP; ++m) tw[u][m] = rw[u][m] = T(0);
+  auto load_blk = [&](int64_t b, V (&tv)[KT], V (&yv)[KT]) {
 #pragma unroll
     for (int u = 0; u < KT; ++u) {
       const int64_t p = p0 + b * KT + u, pr = p - off;
       const bool tin_ok = p >= 0 && p < nsub, y_ok = pr >= lo && pr < hi;
-      const T a = tin[(tin_ok ? p : 0) * plane + pos];
-      const T c = y[(y_ok ? pr : lo) * plane + pos];
-      tv[u] = tin_ok ? a : T(0);
-      yv[u] = y_ok ? c : T(0);
+      const V a = *reinterpret_cast<const V*>(tin + (tin_ok ? p : 0) * plane + pos);
+      const V c = *reinterpret_cast<const V*>(y + (y_ok ? pr : lo) * plane + pos);
+#pragma unroll
+      for (int m = 0; m < VP; ++m) {
+        tv[u].v[m] = tin_ok ? a.v[m] : T(0);
+        yv[u].v[m] = y_ok ? c.v[m] : T(0);
+      }
     }
   };
   if (nblk > 0) load_blk(0, tl, yl);
   for (int64_t b = 0; b < nblk; ++b) {
-    T tn[KT], yn[KT];
+    V tn[KT], yn[KT];
     if (b + 1 < nblk) load_blk(b + 1, tn, yn);
 #pragma unroll
     for (int u = 0; u < KT; ++u) {
       const int64_t p = p0 + b * KT + u, pr = p - off, q = p - k + 1;
-      tw[u] = tl[u];
-      T acc = T(0);
+      V out;
 #pragma unroll
-      for (int t = 0; t < KT; ++t) acc += h[t] * tw[(u - t + KT) % KT];
-      rw[u] = (pr >= lo && pr < hi) ? acc - yl[u] : T(0);
-      T sacc = T(0);
+      for (int m = 0; m < VP; ++m) {
+        tw[u][m] = tl[u].v[m];
+        T acc = T(0);
 #pragma unroll
-      for (int t = 0; t < KT; ++t) sacc += hf[t] * rw[(u - t + KT) % KT];
-      if (q >= q0 && q < q1) s[q * plane + pos] = sacc;
+        for (int t = 0; t < KT; ++t) acc += h[t] * tw[(u - t + KT) % KT][m];
+        rw[u][m] = (pr >= lo && pr < hi) ? acc - yl[u].v[m] : T(0);
+        T sacc = T(0);
+#pragma unroll
+        for (int t = 0; t < KT; ++t) sacc += hf[t] * rw[(u - t + KT) % KT][m];
+        out.v[m] = sacc;
+      }
+      if (q >= q0 && q < q1) *reinterpret_cast<V*>(s + q * plane + pos) = out;
     }
     if (b + 1 < nblk) {
 #pragma unroll
@@ -332,6 +349,12 @@ __global__ __launch_bounds__(256) void k_conv0_rta(const T* __restrict__ tin, co
   }
 }
 
+// fp32 voxels per thread of the axis-0 pass (diagnostics builds override): 2 = 8-B loads / stores, 512 voxels
+// (2 KB) of a plane per workgroup
+#ifndef PCS_CONV0_VP32
+#define PCS_CONV0_VP32 2
+#endif
+
 template <typename T>
 static int conv0_rta(const void* t, const void* y, void* s, int64_t nsub, int64_t plane, const void* taps, int k, int off,
                      int64_t img_lo, int64_t img_hi, int64_t q0, int64_t q1, hipStream_t st) {
@@ -339,13 +362,26 @@ static int conv0_rta(const void* t, const void* y, void* s, int64_t nsub, int64_
       q1 > nsub || q0 > q1)
     return PCS_EINVAL;
   if (q0 == q1) return PCS_OK;
-  const unsigned g = (unsigned)((plane + 255) / 256);
-  if (k <= 7)
-    k_conv0_rta<T, 7><<<g, 256, 0, st>>>((const T*)t, (const T*)y, (T*)s, nsub, plane, (const T*)taps, k, off, img_lo,
-                                         img_hi, q0, q1);
-  else
-    k_conv0_rta<T, kC1K><<<g, 256, 0, st>>>((const T*)t, (const T*)y, (T*)s, nsub, plane, (const T*)taps, k, off,
-                                            img_lo, img_hi, q0, q1);
+  constexpr int VPW = sizeof(T) == 4 ? PCS_CONV0_VP32 : 1;
+  const bool wide = VPW > 1 && plane % VPW == 0 && ((uintptr_t)t | (uintptr_t)y | (uintptr_t)s) % (VPW * sizeof(T)) == 0;
+  const int vp = wide ? VPW : 1;
+  const unsigned g = (unsigned)((plane / vp + 255) / 256);
+  auto go = [&](auto kt, auto vpc) {
+    constexpr int KT = decltype(kt)::value, VP = decltype(vpc)::value;
+    k_conv0_rta<T, KT, VP><<<g, 256, 0, st>>>((const T*)t, (const T*)y, (T*)s, nsub, plane, (const T*)taps, k, off,
+                                              img_lo, img_hi, q0, q1);
+  };
+  using K7 = std::integral_constant<int, 7>;
+  using K15 = std::integral_constant<int, kC1K>;
+  using V1 = std::integral_constant<int, 1>;
+  using VW = std::integral_constant<int, VPW>;
+  if (k <= 7) {
+    if (wide) go(K7{}, VW{});
+    else go(K7{}, V1{});
+  } else {
+    if (wide) go(K15{}, VW{});
+    else go(K15{}, V1{});
+  }
   return launch_status();
 }
 
