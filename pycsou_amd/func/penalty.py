@@ -154,18 +154,22 @@ class L21Norm(LpNorm):
         ss.index_add_(0, self._gid_dev().long(), t.double() ** 2)
         return float(torch.sqrt(ss).sum())
 
+    @staticmethod
+    def _csr_host(inv, ngroups):
+        """(order, offsets, largest group) of group indices `inv`: the elements group by group in ascending
+        element order (a stable argsort), group g at order[off[g]:off[g + 1]]."""
+        order = np.argsort(inv, kind='stable').astype(np.int32)
+        counts = np.bincount(inv, minlength=ngroups)
+        off = np.zeros(counts.size + 1, dtype=np.int64)
+        np.cumsum(counts, out=off[1:])
+        return order, off, int(counts.max()) if counts.size else 0
+
     def _csr_dev(self):
-        """(order, offsets, largest group) of the labels on the device: the elements group by group in
-        ascending element order, for the deterministic group sums of pcs_prox_l21_groups."""
+        """_csr_host of the labels on the device, for the deterministic group sums of pcs_prox_l21_groups."""
         if getattr(self, '_csr', None) is None:
             gid = self._gid_dev()
-            inv = self._inv
-            order = np.argsort(inv, kind='stable').astype(np.int32)
-            counts = np.bincount(inv, minlength=self.groups_idxs.size)
-            off = np.zeros(counts.size + 1, dtype=np.int64)
-            np.cumsum(counts, out=off[1:])
-            self._csr = (torch.as_tensor(order).to(gid.device), torch.as_tensor(off).to(gid.device),
-                         int(counts.max()) if counts.size else 0)
+            order, off, maxlen = self._csr_host(self._inv, self.groups_idxs.size)
+            self._csr = (torch.as_tensor(order).to(gid.device), torch.as_tensor(off).to(gid.device), maxlen)
         return self._csr
 
     def _prox(self, t, tau):

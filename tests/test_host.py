@@ -425,3 +425,18 @@ def test_graft_build_entry():
     ABI the bindings expect -- a stale constant there failed it silently for part of round 6."""
     import __graft_entry__ as g
     g.build()
+
+
+def test_l21_label_groups_csr():
+    """The host side of pcs_prox_l21_groups: every group's members in ascending element order, the
+    offsets of the groups in that list and the largest group (penalty.py:525-560 groups by np.unique)."""
+    import numpy as np
+    from pycsou_amd.func.penalty import L21Norm
+    rng = np.random.default_rng(0)
+    labels = rng.integers(0, 40, 1000) * 7 + 3  # arbitrary label values, some unused
+    uniq, inv = np.unique(labels, return_inverse=True)
+    order, off, maxlen = L21Norm._csr_host(inv, uniq.size)
+    assert off[0] == 0 and off[-1] == labels.size and maxlen == np.bincount(inv).max()
+    for g in range(uniq.size):
+        members = order[off[g]:off[g + 1]]
+        np.testing.assert_array_equal(members, np.flatnonzero(inv == g))  # ascending element order
